@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: disparity-pixels/s of the SAD block matcher on MI355X.
+
+Workload (BASELINE.json configs[2], "C"): 1920x1080 u8 synthetic rectified
+pair, 11x11 SAD, 128 disparities, plus the fused per-pixel distance map (cm,
+f64) -- one "step" = one pair through the hot path with inputs resident in
+HBM.  N GPUs = weak scaling (config D at N=8): every rank owns one pair per
+step (independent, no data-path collective) and rank 0 gathers the u8
+disparity maps over RCCL (xGMI), overlapped with the next step's compute.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+
+Prints ONE JSON line on rank 0 (the driver's contract) with "roofline" for
+the dominant kernel (HBM algorithmic bytes / avg kernel time, HIP events on
+the kernel's stream) and, at N=1, "cpu_baseline" (the C oracle's
+multithreaded sliding-window variant on a bounded row band of the same pair).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from unsynchronized_stereo_vision_proj325_amd import StereoBlockMatcher  # noqa: E402
+from unsynchronized_stereo_vision_proj325_amd.synthetic import synthetic_pair  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (32-bit VALU, MI355X_MICROARCH.md)
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--disparities", type=int, default=128)
+    p.add_argument("--window", type=int, default=11)
+    p.add_argument("--no-distance", action="store_true", help="disparity map only (no fused distance map)")
+    p.add_argument("--gather", choices=["overlap", "sync", "none"], default="overlap")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget (N=1 only)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def traffic_from_profiles(workload_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one exists for this workload."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        e = d.get(workload_key)
+        if e:
+            return float(e["bytes_per_launch"]), e.get("source")
+    except Exception:
+        pass
+    return None, None
+
+
+def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float):
+    """Oracle (oracle/sad_oracle.c sliding variant, all allowed cores) on a bounded row band."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_oracle
+
+    lib = load_oracle()
+    H, W = L.shape
+    cores = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    out = np.zeros_like(L)
+
+    def run(rows):
+        t0 = time.perf_counter()
+        rc = lib.usv_oracle_sad_sliding_rows(L.ctypes.data, R.ctypes.data, W, H, W, D, w, 0,
+                                             out.ctypes.data, W, 0, rows, cores)
+        assert rc == 0
+        return time.perf_counter() - t0
+
+    probe = max(cores, 16)
+    t = run(probe)
+    rows = int(min(H, max(probe, probe * budget_s / max(t, 1e-6) * 0.5)))
+    times = [run(rows) for _ in range(2)]
+    best = min(times)
+    return {
+        "value": rows * W / best,
+        "unit": "disparity-pixels/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"oracle sliding-window SAD, rows 0..{rows} of the {W}x{H} w={w} D={D} pair "
+                  f"({rows * W} output pixels), best of {len(times)}",
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, D, w = a.width, a.height, a.disparities, a.window
+    with_dist = not a.no_distance
+    # rank r owns pair r (weak scaling: one pair per rank per step)
+    L, R, _ = synthetic_pair(W, H, D, pair_index=rank, noise=2)
+    Lt = torch.from_numpy(L).to(dev)
+    Rt = torch.from_numpy(R).to(dev)
+    matcher = StereoBlockMatcher(D, w)
+    nbuf = 2
+    disp_bufs = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    dist_bufs = [torch.empty((H, W), dtype=torch.float64, device=dev) for _ in range(nbuf)] if with_dist else None
+    gather_lists = None
+    if world > 1 and rank == 0 and a.gather != "none":
+        gather_lists = [[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(world)]
+                        for _ in range(nbuf)]
+    stream = torch.cuda.current_stream()
+    pending = [None] * nbuf
+
+    def step(i, ev_pair=None):
+        b = i % nbuf
+        if pending[b] is not None:  # the gather that last read this buffer must finish first
+            pending[b].wait()
+            pending[b] = None
+        if ev_pair is not None:
+            ev_pair[0].record(stream)
+        matcher.compute(Lt, Rt, with_distance=with_dist, out_disp=disp_bufs[b],
+                        out_dist=dist_bufs[b] if with_dist else None)
+        if ev_pair is not None:
+            ev_pair[1].record(stream)
+        if world > 1 and a.gather != "none":
+            work = dist.gather(disp_bufs[b], gather_lists[b] if rank == 0 else None, dst=0,
+                               async_op=True)
+            if a.gather == "sync":
+                work.wait()
+            else:
+                pending[b] = work
+
+    for i in range(a.warmup):
+        step(i)
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i, events[i])
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in events]))
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    pixels = W * H
+    value = world * a.steps * pixels / elapsed
+    bytes_per_px = 3 + (8 if with_dist else 0)  # L + R + u8 disparity (+ f64 distance)
+    alg_bytes = bytes_per_px * pixels
+    achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
+    workload_key = f"C_{W}x{H}_w{w}_D{D}_{'dist' if with_dist else 'nodist'}"
+    traffic, traffic_src = traffic_from_profiles(workload_key)
+    # sliding-window VALU work of the fast kernel: ~7.3 lane-ops per (pixel, disparity)
+    valu_ops = 7.3 * pixels * D
+    rec = {
+        "metric": "disparity-pixels/s (1920x1080, 11x11 SAD, 128 disparities)",
+        "value": value,
+        "unit": "disparity-pixels/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded uniform u8 L, slab-shifted R with +-2 noise; SURVEY.md 8(d))",
+        "config": {
+            "workload": f"C: {W}x{H} u8 rectified pair, {w}x{w} SAD, D={D}, argmin u8 disparity"
+                        + (" + fused f64 distance map (P/DistanceCalculator.cpp:84)" if with_dist else ""),
+            "pairs_per_step": world,
+            "parallelism": f"one pair per GPU, rank-0 RCCL gather of u8 disparity ({a.gather})"
+                           if world > 1 else "single GPU",
+        },
+        "disparity_evals_per_s": value * D,
+        "kernel_ms": kern_ms,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "kernel": "sad_fast_kernel<5,2,16>",
+            "note": "fused kernel is VALU-integer bound (SURVEY.md 8(d)); see valu_roofline",
+        },
+        "valu_roofline": {
+            "achieved_lane_ops_per_s": valu_ops / (kern_ms * 1e-3),
+            "peak": VALU_PEAK_LANE_OPS,
+            "frac": valu_ops / (kern_ms * 1e-3) / VALU_PEAK_LANE_OPS,
+            "ops_model": "7.3 VALU lane-ops per (pixel, disparity), counted from the kernel ISA",
+        },
+    }
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
+        rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+/*
+ * usv_oracle.h -- CPU ORACLE for the stereo block-match / distance hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libusv.so, the Python
+ * package) links, imports or calls this.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load liboracle.so, and only as the
+ * checker / the timed CPU baseline.
+ *
+ * What it restates (reference = /root/reference, P/ = Unsynchronized_Stereo_Vision_Proj325/):
+ *   - SAD/SSD block match + argmin.  The reference has NO
+ *     per-pixel block matcher; the spec is the build's own.
+ *     Nearest reference primitive: absdiff, P/Main.cpp:304.  Parity for this
+ *     function means "bit-exact vs this naive restatement", pinned by
+ *     known-answer tests (shifted synthetic pairs) and an independent
+ *     pure-Python restatement in tests/.
+ *   - per-object distance power law P/DistanceCalculator.cpp:84,
+ *     constant-acceleration extrapolation P/DistanceCalculator.cpp:53-81,
+ *     Canny-path distance P/Main.cpp:681-694, XYZ P/DistanceCalculator.cpp:90-141.
+ *     Pinned against the golden values SURVEY.md §8(c) recorded from the
+ *     reference's own functions (tests/golden/distance_golden.json).
+ *   - ResolveMatchList P/Main.cpp:432-477 and IDMatcher P/Main.cpp:483-499,
+ *     pinned by the SURVEY.md §8(c) golden vectors (duplicate-emitting
+ *     conflict pass; comma-operator Point3i).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#ifndef USV_ORACLE_H
+#define USV_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { USV_ORACLE_SAD = 0, USV_ORACLE_SSD = 1 };
+
+/* A1, definition-level triple loop.  O(W*H*D*w^2).  Returns 0 on success. */
+int usv_oracle_sad_naive(const uint8_t* L, const uint8_t* R, int W, int H, int pitch,
+                         int D, int w, int metric, uint8_t* disp, int disp_pitch);
+
+/* A1, separable running sums, n_threads row bands (0 = all cores).  Must equal
+ * the naive variant bit for bit.  This is the timed CPU baseline. */
+int usv_oracle_sad_sliding(const uint8_t* L, const uint8_t* R, int W, int H, int pitch,
+                           int D, int w, int metric, uint8_t* disp, int disp_pitch,
+                           int n_threads);
+
+/* Same as the sliding variant but only for output rows [y0, y1): bounded CPU sample. */
+int usv_oracle_sad_sliding_rows(const uint8_t* L, const uint8_t* R, int W, int H, int pitch,
+                                int D, int w, int metric, uint8_t* disp, int disp_pitch,
+                                int y0, int y1, int n_threads);
+
+/* P/DistanceCalculator.cpp:84 for one integer disparity (cm; disp 0 -> inf). */
+double usv_oracle_distance_cm(int disp);
+/* P/Main.cpp:694 Canny-path formula for one integer disparity (cm). */
+double usv_oracle_canny_distance_cm(int disp);
+
+/* Per-pixel distance map from a u8 disparity map. */
+void usv_oracle_disparity_to_distance_cm(const uint8_t* disp, int W, int H, int disp_pitch,
+                                         double* out, int out_pitch_elems);
+
+/* P/DistanceCalculator.cpp:15-88 restated over plain arrays.
+ *   pts arrays are interleaved float (x,y); triples are int (x,y,z);
+ *   time stamps are steady_clock tick counts (nanoseconds).
+ *   interp_in/n_interp_in: the caller's InterpolatedVectorCenter_pointOtherCamera
+ *   (by value in the reference; usually empty).  Appends n_triples doubles to
+ *   dist_out (if the three other-camera vectors are non-empty) and returns the
+ *   count appended. */
+int usv_oracle_moving_object_distance(int camera_side_left,
+                                      int64_t ts_this,
+                                      const float* this_pts, int n_this,
+                                      const float* cur_pts, int n_cur,
+                                      const float* old_pts, int n_old,
+                                      const float* older_pts, int n_older,
+                                      const float* interp_in, int n_interp_in,
+                                      const int* triples, int n_triples,
+                                      int64_t ts_other, int64_t ts_other_old,
+                                      int64_t ts_other_older,
+                                      double* dist_out);
+
+/* P/DistanceCalculator.cpp:90-141; xyz_out gets 3 doubles per emitted point.
+ * coordinate_display mirrors the global CoordinateDisplay (P/DistanceCalculator.cpp:6). */
+int usv_oracle_coordinate_position(int camera_side_left, const double* dist, int n_dist,
+                                   const float* this_pts, int n_this,
+                                   int coordinate_display, double* xyz_out);
+
+/* Match record, layout of P/Match.hpp:4-12 (unsigned, unsigned, double). */
+typedef struct { unsigned left, right; double value; } usv_oracle_match;
+
+/* P/Main.cpp:432-477; returns the number of tentative matches written. */
+int usv_oracle_resolve_match_list(const usv_oracle_match* in, int n_in, usv_oracle_match* out);
+/* P/Main.cpp:483-499; out gets 3 ints per triple; returns the triple count. */
+int usv_oracle_id_matcher(const usv_oracle_match* cur, int n_cur,
+                          const usv_oracle_match* old, int n_old, int* out_xyz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

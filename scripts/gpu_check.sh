@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU-box validation run: smoke, parity tests, a short bench.  Each GPU step has
+# its own time limit; a crash / fault / timeout stops the script (no retries).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+fatal() { case "$1" in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
+  return $rc
+}
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+step bench 300 python bench.py --steps 50 --warmup 10
+exit 0

@@ -1,0 +1,169 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) vs the CPU oracle.
+
+Bit-exact on integer outputs (disparity maps) and on the distance map (a
+table gather of the reference's double formula).  Sizes cover BASELINE.json's
+configs A-C at full size, E at full size, and ragged / edge shapes.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle_lib import load_oracle, oracle_sad
+from unsynchronized_stereo_vision_proj325_amd import StereoBlockMatcher, _lib, disparity_to_distance
+from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm
+from unsynchronized_stereo_vision_proj325_amd.synthetic import expected_known_answer, synthetic_pair
+from test_oracle import _fixtures
+
+pytestmark = pytest.mark.gpu
+THREADS = 16  # the box's CPU share
+
+
+def gpu_disp(dev, L, R, D, w, metric="sad", kernel="auto", with_distance=False):
+    Lt = torch.from_numpy(np.ascontiguousarray(L)).to(dev)
+    Rt = torch.from_numpy(np.ascontiguousarray(R)).to(dev)
+    m = StereoBlockMatcher(D, w, metric, kernel=kernel)
+    out = m.compute(Lt, Rt, with_distance=with_distance)
+    torch.cuda.synchronize()
+    if with_distance:
+        return out[0].cpu().numpy(), out[1].cpu().numpy()
+    return out.cpu().numpy()
+
+
+def _mismatch(a, b):
+    bad = np.argwhere(a != b)
+    return f"{len(bad)} mismatches, first at {bad[:5].tolist()}" if len(bad) else ""
+
+
+@pytest.mark.parametrize("case", _fixtures(), ids=lambda c: c[0])
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
+def test_committed_fixtures(gpu, case, kernel):
+    name, L, R, disp, p = case
+    W, H, D, w, m = (int(v) for v in p)
+    got = gpu_disp(gpu, L, R, D, w, "sad" if m == 0 else "ssd", kernel)
+    assert np.array_equal(got, disp), _mismatch(got, disp)
+
+
+@pytest.mark.parametrize("W,H,D,w", [(320, 240, 32, 5), (640, 480, 64, 7), (1920, 1080, 128, 11)],
+                         ids=["configA", "configB", "configC"])
+def test_baseline_configs_full_size(gpu, W, H, D, w):
+    L, R, dstar = synthetic_pair(W, H, D, pair_index=1, noise=2)
+    got = gpu_disp(gpu, L, R, D, w, kernel="fast")
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+
+
+def test_config_e_full_size(gpu):
+    """3840x2160, 15x15, D=256 (four waves per tile, K=16 tiles)."""
+    L, R, dstar = synthetic_pair(3840, 2160, 256, pair_index=2)
+    got = gpu_disp(gpu, L, R, 256, 15, kernel="fast")
+    ref = oracle_sad(L, R, 256, 15, "sad", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    exp = expected_known_answer(dstar, 15)
+    known = exp >= 0
+    assert np.array_equal(got[known], exp[known].astype(np.uint8))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_ragged_shapes_and_disparity_counts(gpu, seed):
+    rng = np.random.default_rng(100 + seed)
+    W = int(rng.integers(1, 260))
+    if seed % 2 == 0:  # pitch % 4 == 0 -> the fast kernel; odd widths take the generic one
+        W = max(4, W - W % 4)
+    H = int(rng.integers(1, 90))
+    D = int(rng.choice([1, 2, 5, 31, 63, 64, 65, 100, 127, 128, 129, 191, 256]))
+    w = int(rng.choice([3, 5, 7, 9, 11, 13, 15]))
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    if seed % 3 == 0:  # low-entropy images: many exact ties, exercises the smallest-d rule
+        L //= 64
+        R //= 64
+    got = gpu_disp(gpu, L, R, D, w)
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
+
+
+@pytest.mark.parametrize("W,H,D,w,metric", [(97, 41, 48, 5, "ssd"), (130, 20, 70, 9, "ssd"),
+                                            (64, 33, 17, 21, "sad"), (50, 17, 9, 1, "sad"),
+                                            (75, 30, 40, 31, "ssd")])
+def test_generic_kernel(gpu, W, H, D, w, metric):
+    rng = np.random.default_rng(W + H)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    got = gpu_disp(gpu, L, R, D, w, metric)
+    ref = oracle_sad(L, R, D, w, metric, "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+
+
+def test_pitched_views(gpu):
+    rng = np.random.default_rng(9)
+    big_L = torch.from_numpy(rng.integers(0, 256, (70, 300), dtype=np.uint8)).to(gpu)
+    big_R = torch.from_numpy(rng.integers(0, 256, (70, 300), dtype=np.uint8)).to(gpu)
+    Lv, Rv = big_L[3:63, 8:208], big_R[3:63, 8:208]  # pitch 300, offset 8 (4-aligned)
+    got = StereoBlockMatcher(80, 7).compute(Lv, Rv).cpu().numpy()
+    ref = oracle_sad(Lv.cpu().numpy(), Rv.cpu().numpy(), 80, 7, "sad", "naive")
+    assert np.array_equal(got, ref)
+    Lu, Ru = big_L[3:63, 5:205], big_R[3:63, 5:205]  # unaligned -> generic kernel
+    got = StereoBlockMatcher(80, 7).compute(Lu, Ru).cpu().numpy()
+    ref = oracle_sad(Lu.cpu().numpy(), Ru.cpu().numpy(), 80, 7, "sad", "naive")
+    assert np.array_equal(got, ref)
+
+
+def test_batch_launch(gpu):
+    pairs = [synthetic_pair(333, 97, 100, pair_index=i) for i in range(3)]
+    L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    R = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    disp, dist = StereoBlockMatcher(100, 9).compute(L, R, with_distance=True)
+    disp = disp.cpu().numpy()
+    lut = distance_lut_cm()
+    for i, (l, r, _) in enumerate(pairs):
+        ref = oracle_sad(l, r, 100, 9, "sad", "sliding", threads=THREADS)
+        assert np.array_equal(disp[i], ref)
+    assert np.array_equal(dist.cpu().numpy(), lut[disp])
+
+
+def test_fused_distance_bitexact(gpu):
+    L, R, _ = synthetic_pair(1920, 1080, 128, pair_index=3)
+    disp, dist = gpu_disp(gpu, L, R, 128, 11, with_distance=True)
+    ora = load_oracle()
+    lut_ref = np.array([ora.usv_oracle_distance_cm(d) for d in range(256)])
+    ref = lut_ref[disp]
+    same = (dist == ref) | (np.isinf(dist) & np.isinf(ref))
+    assert same.all()
+    assert np.isinf(dist[disp == 0]).all()  # disp 0 -> +inf, propagated, not clamped
+
+
+def test_disparity_to_distance_kernel(gpu):
+    rng = np.random.default_rng(4)
+    for H, W in [(1, 1), (7, 33), (480, 640), (1080, 1920)]:
+        d = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(gpu)
+        for model in ("moving_object", "canny"):
+            out = disparity_to_distance(d, model).cpu().numpy()
+            ref = distance_lut_cm(model)[d.cpu().numpy()]
+            assert (((out == ref) | (np.isinf(out) & np.isinf(ref))).all())
+
+
+def test_fast_kernel_refuses_ssd(gpu):
+    L = torch.zeros((16, 16), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.UsvError):
+        StereoBlockMatcher(8, 5, "ssd", kernel="fast").compute(L, L)
+
+
+def test_cpu_tensors_rejected():
+    L = torch.zeros((16, 16), dtype=torch.uint8)
+    with pytest.raises(ValueError):
+        StereoBlockMatcher(8, 5).compute(L, L)
+
+
+def test_deterministic_and_stream_ordered(gpu):
+    L, R, _ = synthetic_pair(1920, 1080, 128, pair_index=5)
+    Lt, Rt = torch.from_numpy(L).to(gpu), torch.from_numpy(R).to(gpu)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    m = StereoBlockMatcher(128, 11)
+    with torch.cuda.stream(s):
+        a = m.compute(Lt, Rt, stream=s)
+        b = m.compute(Lt, Rt, stream=s)
+    s.synchronize()
+    assert torch.equal(a, b)

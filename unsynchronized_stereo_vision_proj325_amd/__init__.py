@@ -1,0 +1,12 @@
+"""MI355X (gfx950) stereo block-match + distance engine.
+
+Drop-in for the hot path of 6dwavenminer/Unsynchronized_Stereo_Vision_Proj325:
+the per-pixel SAD/SSD disparity search (new) and the
+reference's distance / matcher API (Match.hpp, DistanceCalculator.hpp).
+Compute runs in libusv.so (hand-written HIP for gfx950 behind a C ABI,
+include/usv.h); this package is the Python host layer used by tests and bench.
+"""
+from . import _lib  # noqa: F401
+from .engine import StereoBlockMatcher, disparity_to_distance, distance_lut_cm, sad_disparity  # noqa: F401
+
+__all__ = ["StereoBlockMatcher", "sad_disparity", "disparity_to_distance", "distance_lut_cm"]

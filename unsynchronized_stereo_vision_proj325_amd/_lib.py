@@ -1,0 +1,100 @@
+"""ctypes binding of libusv.so (include/usv.h).
+
+The shared library is built in-tree (``make -C unsynchronized_stereo_vision_proj325_amd/csrc``,
+or ``__graft_entry__.build()``) and loaded from this package directory.  There is
+no fallback: if the library is missing every entry point raises, so a GPU run
+can never silently take a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint8, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libusv.so")
+
+USV_OK = 0
+USV_ERR_INVALID_ARG = 1
+USV_ERR_UNSUPPORTED = 2
+USV_ERR_HIP = 3
+USV_ERR_NO_DEVICE = 4
+STATUS_NAMES = {
+    USV_OK: "USV_OK",
+    USV_ERR_INVALID_ARG: "USV_ERR_INVALID_ARG",
+    USV_ERR_UNSUPPORTED: "USV_ERR_UNSUPPORTED",
+    USV_ERR_HIP: "USV_ERR_HIP",
+    USV_ERR_NO_DEVICE: "USV_ERR_NO_DEVICE",
+}
+
+METRIC_SAD, METRIC_SSD = 0, 1
+DIST_MOVING_OBJECT, DIST_CANNY = 0, 1
+KERNEL_AUTO, KERNEL_FAST, KERNEL_GENERIC = 0, 1, 2
+
+
+class UsvError(RuntimeError):
+    def __init__(self, func: str, status: int):
+        super().__init__(f"{func} failed: {STATUS_NAMES.get(status, status)}")
+        self.status = status
+
+
+class usv_match(ctypes.Structure):
+    """Layout of P/Match.hpp:4-12 (unsigned, unsigned, double)."""
+
+    _fields_ = [("left_index", ctypes.c_uint), ("right_index", ctypes.c_uint), ("match_value", c_double)]
+
+
+# name -> (restype, argtypes); every symbol include/usv.h declares.
+SIGNATURES = {
+    "usv_version": (c_char_p, []),
+    "usv_device_check": (c_int, [POINTER(c_int)]),
+    "usv_sad_disparity": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_void_p, c_int, c_void_p]),
+    "usv_sad_disparity_ex": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "usv_sad_disparity_batch": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_void_p, c_size_t, c_int, c_void_p,
+                                        c_size_t, c_int, c_void_p, c_void_p]),
+    "usv_distance_lut_cm": (c_int, [c_int, POINTER(c_double)]),
+    "usv_disparity_to_distance": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                          c_void_p]),
+    "usv_resolve_match_list": (c_int, [POINTER(usv_match), c_int, POINTER(usv_match), POINTER(c_int)]),
+    "usv_id_matcher": (c_int, [POINTER(usv_match), c_int, POINTER(usv_match), c_int, POINTER(c_int),
+                               POINTER(c_int)]),
+    "usv_generate_matching_list": (c_int, [POINTER(c_int), POINTER(c_int), c_int, POINTER(c_int),
+                                           POINTER(c_int), c_int, POINTER(usv_match), c_int,
+                                           POINTER(c_int)]),
+    "usv_match_shapes_i1": (c_double, [POINTER(c_int), c_int, POINTER(c_int), c_int]),
+    "usv_contour_area": (c_double, [POINTER(c_int), c_int]),
+    "usv_moving_object_distance": (c_int, [c_int, c_int64, POINTER(c_float), c_int, POINTER(c_float),
+                                           c_int, POINTER(c_float), c_int, POINTER(c_float), c_int,
+                                           POINTER(c_int), c_int, c_int64, c_int64, c_int64,
+                                           POINTER(c_double), POINTER(c_float), POINTER(c_int)]),
+    "usv_coordinate_position": (c_int, [c_int, POINTER(c_double), c_int, POINTER(c_float), c_int, c_int,
+                                        POINTER(c_double), POINTER(c_int)]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libusv.so once; raise (never fall back) if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')}` "
+            "or __graft_entry__.build(); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(func: str, status: int) -> None:
+    if status != USV_OK:
+        raise UsvError(func, status)
