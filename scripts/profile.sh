@@ -1,0 +1,28 @@
+#!/bin/bash
+# rocprofv3 passes over a short bench run (GPU box).  Kernel trace + stats in
+# one pass; every PMC group in its own pass (no tracing domains beside --pmc).
+# Output: gpurun_out/prof_<tag>/...  Usage: scripts/profile.sh <tag> [bench args]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+TAG=${1:-r01}; shift
+ARGS=${*:---steps 20 --warmup 5 --no-cpu-baseline}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+fatal() { case "$1" in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
+run() {  # run <name> <rocprofv3 args...>
+  local name=$1; shift
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 240 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS \
+     > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 3 $OUT/$name.log
+  if fatal $rc; then echo "FATAL rc=$rc in $name"; exit $rc; fi
+}
+rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+run trace --kernel-trace --stats
+run pmc_fetch --pmc FETCH_SIZE
+run pmc_write --pmc WRITE_SIZE
+run pmc_inst --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH
+run pmc_cyc --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT
+run pmc_grbm --pmc GRBM_GUI_ACTIVE GRBM_COUNT
+exit 0

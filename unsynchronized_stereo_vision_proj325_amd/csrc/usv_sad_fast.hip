@@ -7,8 +7,8 @@
 // Mapping (DESIGN.md §3 has the derivation):
 //   * lane = disparity.  A workgroup is NW waves; lane l of wave w owns
 //     d = NW*l + w, so the L operand is uniform across the wave (SGPRs) and
-//     only R is gathered per lane.  Lanes with d >= D duplicate d = D-1, which
-//     cannot change the argmin (equal key).
+//     only R is gathered per lane.  Lanes with d >= D replay the wave's last
+//     valid disparity (same data, same key), which cannot change the argmin.
 //   * one workgroup = one x-tile of K outputs x one band of rows, walking down
 //     the band.  Per input row each lane runs a horizontal prefix chain over
 //     K + 2r columns with v_sad_u8 (one instruction per |L-R| + accumulate),
@@ -149,12 +149,15 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
                                           int wave, int x0, int y_begin, int y_end) {
     using C = Cfg<RAD, NW, K>;
     constexpr int WIN = C::WIN;
-    const int d_eff = min(NW * lane + wave, a.D - 1);
+    // Lanes past D-1 replay the last valid lane of this wave (same R column
+    // alignment, same key), so they can never change the argmin.
+    const int l_eff = min(lane, (a.D - 1 - wave) / NW);
+    const int d_eff = NW * l_eff + wave;
     const int cbase = x0 - RAD - (NW * 63 + wave);  // first R column this wave stages
     uint32_t* rbuf = smem + C::RBUF_OFF + wave * 2 * C::NRP;
     uint32_t* comb = smem + C::COMB_OFF;
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
-    const int s_l = NW * (63 - lane);  // this lane's first chain entry in rbuf
+    const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in rbuf
     const int nout = y_end - y_begin;
     const int T = nout + 2 * RAD;  // input rows walked
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
