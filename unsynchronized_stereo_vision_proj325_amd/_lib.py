@@ -12,7 +12,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint8, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libusv.so")
+# USV_LIB_PATH: development override (A/B builds of the same C ABI); default in-tree build.
+LIB_PATH = os.environ.get("USV_LIB_PATH") or os.path.join(_HERE, "libusv.so")
 
 USV_OK = 0
 USV_ERR_INVALID_ARG = 1

@@ -4,26 +4,29 @@
 // has no block matcher; its nearest primitive is the u8
 // absdiff motion mask at P/Main.cpp:304.
 //
-// Mapping (DESIGN.md §3 has the derivation):
+// Mapping (DESIGN.md §3 has the derivation and the instruction budget):
 //   * lane = disparity.  A workgroup is NW waves; lane l of wave w owns
 //     d = NW*l + w, so the L operand is uniform across the wave (SGPRs) and
 //     only R is gathered per lane.  Lanes with d >= D replay the wave's last
 //     valid disparity (same data, same key), which cannot change the argmin.
-//   * one workgroup = one x-tile of K outputs x one band of rows, walking down
-//     the band.  Per input row each lane runs a horizontal prefix chain over
-//     K + 2r columns with v_sad_u8 (one instruction per |L-R| + accumulate),
-//     giving the row-window sums H[x] = B[x+w] - B[x].
-//   * the vertical window is a running sum S += H(new row) - H(row w back);
-//     the w rows of H history live in a packed-u16 register ring (H <= 57375
-//     for w <= 15), rotated statically by unrolling the row loop w times.
-//   * S is kept as a key (cost << 8) | d, so the argmin over disparities is a
-//     plain unsigned min and the smallest d wins ties by construction.
-//   * the min over the 64 lanes of K pixels is a transpose-reduction
-//     (permlane32_swap, permlane16_swap, then DPP mirror rounds): ~2.2 VALU
-//     instructions per pixel-disparity instead of 6 for per-pixel reductions.
-//   * per-wave R rows are staged to LDS as one u32 per column (lane-linear
-//     b64/b128 reads need no per-lane alignment fix-up with the d = NW*l + w
-//     interleave); loads for row t+2 are in flight while row t computes.
+//   * one workgroup = one x-tile of K = 16 outputs x one band of rows, walking
+//     down the band.  Per input row each lane runs a horizontal prefix chain
+//     packed two-per-register: the low half accumulates columns x, the high
+//     half columns x + K/2 (v_sad_u8 / v_sad_hi_u8: one |L-R| + accumulate
+//     each), so the row-window sums of two outputs come from one packed
+//     subtraction H = P[x+w] - P[x].
+//   * the vertical window is a running sum S += H(new row) - H(row w back) in
+//     packed u16 (the cost of a 15x15 SAD window is <= 57375); the w rows of H
+//     history live in a register ring rotated statically by unrolling the row
+//     loop w times.
+//   * argmin: keys (cost << 8) | d are assembled with one v_perm per pixel,
+//     then the min over the 64 lanes of the 16 pixels is a transpose-reduction
+//     (permlane32_swap, permlane16_swap, DPP mirror rounds); the smallest d
+//     wins ties by construction.
+//   * R rows are staged by LDS-DMA (global_load_lds_ubyte writes one u32 per
+//     column) into a per-wave ring of NB row buffers, PD rows ahead, so input
+//     latency is hidden without registers; L rows come through the scalar
+//     cache one row ahead (edge tiles, which clamp, DMA them too).
 //   * the NW waves' partial minima are combined through LDS every kRB rows.
 // Integer arithmetic only: bit-exact with the oracle by construction.
 #include <type_traits>
@@ -35,30 +38,45 @@ namespace usv {
 namespace {
 
 constexpr int kRB = 8;  // output rows buffered between cross-wave combines
-#ifndef USV_FAST_K
-#define USV_FAST_K 16  // outputs per x-tile (16 or 32)
+constexpr int kK = 16;  // outputs per x-tile
+#ifndef USV_FAST_OCC
+#define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__): 3 -> <= 168 VGPRs
 #endif
 
-template <int RAD, int NW, int K>
+using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+
+template <int RAD, int NW>
 struct Cfg {
+    static constexpr int K = kK;
+    static constexpr int HALF = K / 2;
     static constexpr int WIN = 2 * RAD + 1;
-    static constexpr int NPOS = K + 2 * RAD;             // chain positions per input row
-    static constexpr int NR = NPOS + NW * 63;            // R columns a wave stages per row
+    static constexpr int NPOS = K + 2 * RAD;    // columns of one input row the tile needs
+    static constexpr int NSTEP = HALF + 2 * RAD;  // packed chain steps
     static constexpr int VEC = NW >= 4 ? 4 : (NW == 2 ? 2 : 1);  // LDS read width (dwords)
     static constexpr int NPOS_V = (NPOS + VEC - 1) / VEC * VEC;
-    static constexpr int NRP = (NW * 63 + NPOS_V + 3) / 4 * 4;  // padded entries per buffer
-    static constexpr int NQ = (NRP + 63) / 64;                  // staging loads per lane
-    static constexpr int NPOSP = (NPOS + 3) / 4 * 4;            // L entries (edge tiles)
-    static constexpr int LOFF = (4 - (RAD & 3)) & 3;            // (x0 - RAD) mod 4, x0 % 4 == 0
-    static constexpr int NLW = (LOFF + NPOS + 3) / 4;           // L dwords (interior tiles)
+    static constexpr int NR = NW * 63 + NPOS_V;  // R entries a wave reads per row
+    static constexpr int NQ = (NR + 63) / 64;    // DMA instructions per R row
+    static constexpr int NRS = NQ * 64;          // row-buffer stride (entries)
+    static constexpr int NB = NW >= 4 ? 4 : 8;   // row buffers per wave
+    static constexpr int PD = NB - 1;            // rows in flight ahead of the one computed
+    static constexpr int NPOSP = NPOS <= 32 ? 32 : 64;  // edge-tile L entries per row (pow2)
+    static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - RAD) mod 4, x0 % 4 == 0
+    static constexpr int NLW = (LOFF + NPOS + 3) / 4;  // L dwords (interior tiles): 6 or 8
+    static_assert(NLW == 6 || NLW == 8, "scalar L segment is 6 or 8 dwords");
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
-    static constexpr int LBUF_OFF = RBUF_OFF + NW * 2 * NRP;
-    static constexpr int COMB_OFF = LBUF_OFF + NW * 2 * NPOSP;
+    static constexpr int LBUF_OFF = RBUF_OFF + NW * NB * NRS;
+    static constexpr int COMB_OFF = LBUF_OFF + NW * NB * NPOSP;
     static constexpr int LUT_OFF = COMB_OFF + 2 * kRB * NW * 64;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
-    static_assert(K == 16 || K == 32, "transpose-reduction is written for K = 16 or 32");
-    static_assert(RAD >= 1 && RAD <= 7, "packed-u16 ring needs w <= 15");
+    static_assert(RAD >= 1 && RAD <= 7, "packed-u16 cost needs w <= 15");
+    static_assert(NPOSP <= 64, "one DMA instruction per edge L row");
 };
 
 template <int CTRL>
@@ -70,56 +88,35 @@ constexpr int kRowHalfMirror = 0x141;
 constexpr int kQuadSwap2 = 0x4E;  // quad_perm [2,3,0,1]
 constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]
 
-// One transposing round at in-row distance S: result lane l holds, for the
-// S-half it sits in, the min over itself and its mirror partner.
-template <int S, int CTRL>
+// One transposing round inside 16-lane rows: lanes of the low half (by the
+// round's bit) keep a's pixel, the high half b's; each takes the min with its
+// mirror partner in the other half.
+template <int CTRL>
 __device__ __forceinline__ uint32_t tr_round(uint32_t a, uint32_t b, bool hi) {
     const uint32_t u = hi ? b : a;
     const uint32_t v = hi ? a : b;
     return min(u, dpp<CTRL>(v));
 }
 
-// Reduce K keys (each a 64-lane vector over disparities) to one register:
-// afterwards lane l holds the minimum key of pixel l / (64 / K).
-template <int K>
-__device__ __forceinline__ uint32_t reduce_keys(const uint32_t (&k)[K], int lane) {
-    const bool h8 = lane & 8, h4 = lane & 4, h2 = lane & 2;
-    if constexpr (K == 32) {
-        uint32_t r1[16], r2[8], r3[4], r4[2];
+// 16 keys (64-lane vectors over disparities) -> lane l holds the min key of pixel l >> 2.
+__device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16], int lane) {
+    const bool h8 = lane & 8, h4 = lane & 4;
+    uint32_t r1[8], r2[4], r3[2];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            auto p = __builtin_amdgcn_permlane32_swap(k[i], k[i + 16], false, false);
-            r1[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // lanes 0-31: pixel i, 32-63: pixel i+16
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            auto p = __builtin_amdgcn_permlane16_swap(r1[i], r1[i + 8], false, false);
-            r2[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 8q
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r3[i] = tr_round<8, kRowMirror>(r2[i], r2[i + 4], h8);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) r4[i] = tr_round<4, kRowHalfMirror>(r3[i], r3[i + 2], h4);
-        const uint32_t r5 = tr_round<2, kQuadSwap2>(r4[0], r4[1], h2);
-        return min(r5, dpp<kQuadSwap1>(r5));  // lane l: pixel l >> 1
-    } else {
-        uint32_t r1[8], r2[4], r3[2];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            auto p = __builtin_amdgcn_permlane32_swap(k[i], k[i + 8], false, false);
-            r1[i] = min((uint32_t)p[0], (uint32_t)p[1]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            auto p = __builtin_amdgcn_permlane16_swap(r1[i], r1[i + 4], false, false);
-            r2[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // row q: pixel i + 4q
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) r3[i] = tr_round<8, kRowMirror>(r2[i], r2[i + 2], h8);
-        uint32_t r4 = tr_round<4, kRowHalfMirror>(r3[0], r3[1], h4);
-        r4 = min(r4, dpp<kQuadSwap2>(r4));
-        return min(r4, dpp<kQuadSwap1>(r4));  // lane l: pixel l >> 2
+    for (int i = 0; i < 8; ++i) {
+        auto p = __builtin_amdgcn_permlane32_swap(k[i], k[i + 8], false, false);
+        r1[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // lanes 0-31: pixel i, 32-63: pixel i+8
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        auto p = __builtin_amdgcn_permlane16_swap(r1[i], r1[i + 4], false, false);
+        r2[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 4q
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r3[i] = tr_round<kRowMirror>(r2[i], r2[i + 2], h8);
+    uint32_t r4 = tr_round<kRowHalfMirror>(r3[0], r3[1], h4);
+    r4 = min(r4, dpp<kQuadSwap2>(r4));
+    return min(r4, dpp<kQuadSwap1>(r4));
 }
 
 template <int VEC> struct VecT;
@@ -134,30 +131,77 @@ __device__ __forceinline__ uint32_t vget(const typename VecT<VEC>::T& v, int e) 
     else return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
 }
 
-__device__ __forceinline__ void wave_lds_fence() {
-    // Same-wave LDS ops execute in order; this only stops the compiler from
-    // moving another lane's reads above this lane's writes.
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+// Wait until at most N vector-memory operations of this wave are outstanding
+// (they retire in issue order, so every older LDS-DMA row has landed).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int RAD, int NW, int K, bool INTERIOR>
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
+// vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
+// stores, so lgkmcnt(0) before the barrier is all the hand-off needs.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Scalar-load an exact number of dwords (6 or 8: no read past the row) into SGPRs.
+template <int N> struct SWords;
+template <> struct SWords<6> {
+    struct T { uint32_t __attribute__((ext_vector_type(4))) a; uint32_t __attribute__((ext_vector_type(2))) b; };
+};
+template <> struct SWords<8> {
+    using T = uint32_t __attribute__((ext_vector_type(8)));
+};
+template <int N>
+__device__ __forceinline__ typename SWords<N>::T s_load_words(const uint8_t* p) {
+    typename SWords<N>::T w;
+    if constexpr (N == 8) {
+        asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(w) : "s"(p) : "memory");
+    } else {
+        asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx2 %1, %2, 0x10"
+                     : "=s"(w.a), "=s"(w.b) : "s"(p) : "memory");
+    }
+    return w;
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm0(typename SWords<N>::T& w) {
+    if constexpr (N == 8) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w) : : "memory");
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w.a), "+s"(w.b) : : "memory");
+    }
+}
+template <int N>
+__device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uint32_t (&o)[8]) {
+    if constexpr (N == 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = w[i];
+    } else {
+        o[0] = w.a[0]; o[1] = w.a[1]; o[2] = w.a[2]; o[3] = w.a[3];
+        o[4] = w.b[0]; o[5] = w.b[1]; o[6] = 0; o[7] = 0;
+    }
+}
+
+template <int RAD, int NW, bool INTERIOR>
 __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
                                           const uint8_t* __restrict__ R,
                                           uint8_t* __restrict__ disp, double* __restrict__ dist,
                                           const MatchArgs& a, uint32_t* smem, int lane,
                                           int wave, int x0, int y_begin, int y_end) {
-    using C = Cfg<RAD, NW, K>;
-    constexpr int WIN = C::WIN;
-    // Lanes past D-1 replay the last valid lane of this wave (same R column
-    // alignment, same key), so they can never change the argmin.
+    using C = Cfg<RAD, NW>;
+    using LWords = typename SWords<C::NLW>::T;
+    constexpr int WIN = C::WIN, K = C::K, HALF = C::HALF;
+    constexpr int NDMA = C::NQ + (INTERIOR ? 0 : 1);  // VMEM ops issued per input row
     const int l_eff = min(lane, (a.D - 1 - wave) / NW);
-    const int d_eff = NW * l_eff + wave;
+    const uint32_t d_eff = (uint32_t)(NW * l_eff + wave);
     const int cbase = x0 - RAD - (NW * 63 + wave);  // first R column this wave stages
-    uint32_t* rbuf = smem + C::RBUF_OFF + wave * 2 * C::NRP;
+    uint32_t* rbuf = smem + C::RBUF_OFF + wave * C::NB * C::NRS;
+    uint32_t* lbuf = smem + C::LBUF_OFF + wave * C::NB * C::NPOSP;
     uint32_t* comb = smem + C::COMB_OFF;
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
-    const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in rbuf
+    const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
     const int nout = y_end - y_begin;
     const int T = nout + 2 * RAD;  // input rows walked
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
@@ -167,105 +211,101 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         return img + (size_t)y * a.pitch;
     };
 
-    // ---- staging: global -> registers (issue) -> LDS (commit) ----
-    // Edge tiles (border clamping on the L side) build the same dword words as
-    // the interior SGPR path: lane i < NLW packs 4 clamped L bytes, and the row
-    // is moved to SGPRs with v_readlane.
-    uint32_t q[C::NQ];
-    uint32_t ql = 0;
-    auto issue_row = [&](int t) {
+    // ---- R (and edge-tile L) rows: LDS-DMA into the ring, PD rows ahead ----
+    // Rows past the band are clamped to real rows: harmless extra loads.
+    // Clamped source columns do not depend on the row: 32-bit lane offsets
+    // against a scalar row base (the saddr form of the DMA, no 64-bit VGPRs).
+    uint32_t colR[C::NQ];
+#pragma unroll
+    for (int i = 0; i < C::NQ; ++i) colR[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1);
+    const uint32_t colL = (uint32_t)min(max(x0 - RAD + lane, 0), Wm1);
+    auto issue_dma = [&](int t) {
+        const int buf = t & (C::NB - 1);
         const uint8_t* rr = row_ptr(R, t);
 #pragma unroll
-        for (int i = 0; i < C::NQ; ++i) q[i] = rr[min(max(cbase + lane + 64 * i, 0), Wm1)];
+        for (int i = 0; i < C::NQ; ++i)
+            __builtin_amdgcn_global_load_lds(rr + colR[i], rbuf + buf * C::NRS + 64 * i, 1, 0, 0);
         if constexpr (!INTERIOR) {
             const uint8_t* lr = row_ptr(L, t);
-            const int c0 = x0 - RAD - C::LOFF + 4 * lane;
-            ql = 0;
-            if (lane < C::NLW) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) ql |= (uint32_t)lr[min(max(c0 + k, 0), Wm1)] << (8 * k);
-            }
+            if (lane < C::NPOSP)
+                __builtin_amdgcn_global_load_lds(lr + colL, lbuf + buf * C::NPOSP, 1, 0, 0);
         }
-    };
-    auto commit_row = [&](int t) {
-        uint32_t* dst = rbuf + (t & 1) * C::NRP;
-#pragma unroll
-        for (int i = 0; i < C::NQ; ++i)
-            if (C::NRP % 64 == 0 || lane + 64 * i < C::NRP) dst[lane + 64 * i] = q[i];
     };
 
-    // One input row t: chain over the K + 2r columns, and as soon as a
-    // row-window sum H[x] = B[x+w] - B[x] exists fold it into the key S[x] and
-    // the ring slot.  WARM: first w rows (no subtraction).  Consuming H on the
-    // fly keeps the live set at ring + S + a (w+1)-deep chain window.
-    uint32_t lw_next[C::NLW];
+    // ---- L bytes of the interior path: the row segment through the scalar
+    // cache, requested one row ahead.  Issued as inline asm: the compiler
+    // would otherwise turn it into a vector load (the LDS-DMA intrinsic
+    // defeats its no-clobber proof) and drain the DMA look-ahead with
+    // vmcnt(0).  Scalar loads return out of order, so only lgkmcnt(0) can
+    // retire one; the wait takes the words as operands so nothing that reads
+    // them can be scheduled above it.
+    LWords lw_next;
     auto load_lw = [&](int t) {
-        if constexpr (INTERIOR) {
-            const uint32_t* p =
-                reinterpret_cast<const uint32_t*>(row_ptr(L, t) + (x0 - RAD - C::LOFF));
-#pragma unroll
-            for (int i = 0; i < C::NLW; ++i) lw_next[i] = p[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < C::NLW; ++i) lw_next[i] = __builtin_amdgcn_readlane(ql, i);
-        }
+        const uint8_t* p = row_ptr(L, t) + (x0 - RAD - C::LOFF);
+        lw_next = s_load_words<C::NLW>(p);
     };
-    auto do_row = [&](int t, auto warm_tag, auto slot_tag, uint32_t(&S)[K],
-                      uint32_t(&ring)[WIN][K / 2]) {
+    // One input row t: packed chain, H pairs, S / ring update.
+    auto do_row = [&](int t, auto warm_tag, auto slot_tag, uint32_t(&S)[HALF],
+                      uint32_t(&ring)[WIN][HALF]) {
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int SL = decltype(slot_tag)::value;
-        // L operand of this row (uniform, SGPRs): bytes of the dword-aligned segment.
+        const int buf = t & (C::NB - 1);
+        wait_vmcnt<(C::PD - 1) * NDMA>();  // row t has landed in LDS
+        __builtin_amdgcn_wave_barrier();
+        issue_dma(t + C::PD);
+
         uint32_t Lv[C::NPOS];
-        uint32_t lw[C::NLW];
+        if constexpr (INTERIOR) {
+            LWords cur = lw_next;
+            wait_lgkm0<C::NLW>(cur);  // row t's words have arrived
+            load_lw(t + 1);   // and row t+1's are requested a full row ahead
+            uint32_t lw[8];
+            unpack_words<C::NLW>(cur, lw);
 #pragma unroll
-        for (int i = 0; i < C::NLW; ++i) lw[i] = lw_next[i];
+            for (int j = 0; j < C::NPOS; ++j) {
+                const int bidx = C::LOFF + j;
+                Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+            }
+        } else {
+            // lane j holds clamped column j of the segment; move it to SGPRs
+            const uint32_t lcol = lbuf[buf * C::NPOSP + (lane & (C::NPOSP - 1))];
 #pragma unroll
-        for (int j = 0; j < C::NPOS; ++j) {
-            const int bidx = C::LOFF + j;
-            Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+            for (int j = 0; j < C::NPOS; ++j) Lv[j] = __builtin_amdgcn_readlane(lcol, j);
         }
-        // stage row t+1 (loaded a row ago) and put row t+2 in flight
-        if constexpr (!INTERIOR) load_lw(t + 1);  // ql holds row t+1 (issued a row ago)
-        commit_row(t + 1);
-        wave_lds_fence();
-        issue_row(t + 2);
-        if constexpr (INTERIOR) load_lw(t + 1);
 
         using VT = typename VecT<C::VEC>::T;
-        const VT* rb = reinterpret_cast<const VT*>(rbuf + (t & 1) * C::NRP + s_l);
-        uint32_t B[C::NPOS + 1];
-        uint32_t Hlo = 0;
-        B[0] = 0;
+        const VT* rb = reinterpret_cast<const VT*>(rbuf + buf * C::NRS + s_l);
+        uint32_t Rv[C::NPOS_V];
 #pragma unroll
         for (int jv = 0; jv < C::NPOS_V / C::VEC; ++jv) {
             const VT v = rb[jv];
 #pragma unroll
-            for (int e = 0; e < C::VEC; ++e) {
-                const int j = jv * C::VEC + e;
-                if (j < C::NPOS) {
-                    B[j + 1] = __builtin_amdgcn_sad_u8(Lv[j], vget<C::VEC>(v, e), B[j]);
-                    const int x = j + 1 - WIN;  // H[x] complete
-                    if (x >= 0) {
-                        const uint32_t h = B[x + WIN] - B[x];
-                        if constexpr (WARM) {
-                            S[x] += h << 8;
-                        } else {
-                            const uint32_t old = (x & 1) ? (ring[SL][x >> 1] >> 16)
-                                                         : (ring[SL][x >> 1] & 0xFFFFu);
-                            S[x] += (h - old) << 8;
-                        }
-                        if (x & 1) ring[SL][x >> 1] = Hlo | (h << 16);
-                        else Hlo = h;
-                    }
-                }
+            for (int e = 0; e < C::VEC; ++e) Rv[jv * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+        // packed prefix: P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)]
+        uint32_t P[C::NSTEP + 1];
+        P[0] = 0;
+#pragma unroll
+        for (int j = 0; j < C::NSTEP; ++j) {
+            P[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
+                                                  __builtin_amdgcn_sad_u8(Lv[j], Rv[j], P[j]));
+            const int x = j + 1 - WIN;  // H pair (x, x + HALF) complete
+            if (x >= 0 && x < HALF) {
+                const uint32_t h = pk_sub(P[x + WIN], P[x]);
+                if constexpr (WARM) S[x] = pk_add(S[x], h);
+                else S[x] = pk_sub(pk_add(S[x], h), ring[SL][x]);
+                ring[SL][x] = h;
             }
         }
+        // Keep rows apart: interleaving the unrolled warm-up rows only raises
+        // register pressure (spills whose reloads would drain the DMA queue).
+        __builtin_amdgcn_sched_barrier(0);
     };
 
     // ---- output: per-row keys -> LDS, cross-wave min every kRB rows ----
     int slot = 0, cb = 0, y_chunk = y_begin;
     auto flush = [&]() {
-        __syncthreads();
+        lds_barrier();
         const int items = slot * K;
         for (int i = threadIdx.x; i < items; i += NW * 64) {
             const int row = i / K, p = i - row * K;
@@ -285,24 +325,28 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         slot = 0;
         cb ^= 1;
     };
-    auto emit = [&](const uint32_t(&S)[K], bool last) {
-        const uint32_t m = reduce_keys<K>(S, lane);
+    auto emit = [&](const uint32_t(&S)[HALF], bool last) {
+        uint32_t keys[K];
+#pragma unroll
+        for (int i = 0; i < HALF; ++i) {
+            keys[i] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c050400u);         // (S.lo << 8) | d
+            keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
+        }
+        const uint32_t m = reduce16(keys, lane);
         comb[((cb * kRB + slot) * NW + wave) * 64 + lane] = m;
         ++slot;
         if (slot == kRB || last) flush();
     };
 
-    uint32_t S[K];
+    uint32_t S[HALF];
 #pragma unroll
-    for (int x = 0; x < K; ++x) S[x] = (uint32_t)d_eff;
-    uint32_t ring[WIN][K / 2];
+    for (int i = 0; i < HALF; ++i) S[i] = 0;
+    uint32_t ring[WIN][HALF];
 
-    // prologue: row 0 staged, row 1 in flight
-    issue_row(0);
-    load_lw(0);
-    commit_row(0);
-    wave_lds_fence();
-    issue_row(1);
+    // prologue: PD rows in flight, L words of rows 0 and 1 requested
+#pragma unroll
+    for (int t = 0; t < C::PD; ++t) issue_dma(t);
+    if constexpr (INTERIOR) load_lw(0);
 
     using WarmT = std::integral_constant<bool, true>;
     using SteadyT = std::integral_constant<bool, false>;
@@ -322,19 +366,20 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
              ...);
         }(std::make_integer_sequence<int, WIN>{});
     }
+    wait_vmcnt<0>();  // drain the look-ahead DMAs before the wave retires
 }
 
-template <int RAD, int NW, int K>
-__global__ __launch_bounds__(NW * 64, 2) void sad_fast_kernel(const uint8_t* __restrict__ L,
+template <int RAD, int NW>
+__global__ __launch_bounds__(NW * 64, USV_FAST_OCC) void sad_fast_kernel(const uint8_t* __restrict__ L,
                                                               const uint8_t* __restrict__ R,
                                                               uint8_t* __restrict__ disp,
                                                               double* __restrict__ dist,
                                                               MatchArgs a, int band_rows) {
-    using C = Cfg<RAD, NW, K>;
+    using C = Cfg<RAD, NW>;
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x0 = blockIdx.x * K;
+    const int x0 = blockIdx.x * C::K;
     const int y_begin = blockIdx.y * band_rows;
     const int y_end = min(a.H, y_begin + band_rows);
     const size_t b = blockIdx.z;
@@ -347,30 +392,52 @@ __global__ __launch_bounds__(NW * 64, 2) void sad_fast_kernel(const uint8_t* __r
         for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
     }
     __syncthreads();
-    const bool interior = (x0 - RAD >= 0) && (x0 + K - 1 + RAD <= a.W - 1);
+    const bool interior = (x0 - RAD >= 0) && (x0 + C::K - 1 + RAD <= a.W - 1);
     if (interior)
-        band_loop<RAD, NW, K, true>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+        band_loop<RAD, NW, true>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
     else
-        band_loop<RAD, NW, K, false>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+        band_loop<RAD, NW, false>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
 }
 
-template <int RAD>
-constexpr int k_for_rad() { return USV_FAST_K; }
+// Blocks resident per CU for this instantiation (queried once).
+template <int RAD, int NW>
+int resident_blocks_per_cu() {
+    static const int n = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_fast_kernel<RAD, NW>, NW * 64, 0) !=
+                hipSuccess || v <= 0)
+            v = 1;
+        return v;
+    }();
+    return n;
+}
+
+int cu_count() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
 
 template <int RAD, int NW>
 hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
-    constexpr int K = k_for_rad<RAD>();
+    constexpr int K = kK, WIN = 2 * RAD + 1;
     const int n_xt = (a.W + K - 1) / K;
-    // ~2 resident waves per SIMD: 8 waves per CU on 256 CUs.
-    const int target_blocks = 256 * 8 / NW;
-    int n_bands = (target_blocks + n_xt * a.batch - 1) / (n_xt * a.batch);
-    const int min_rows = 4 * (2 * RAD + 1);
-    int band_rows = (a.H + n_bands - 1) / n_bands;
-    if (band_rows < min_rows) band_rows = min_rows;
+    // One round of resident workgroups: bands = slots / (x-tiles * pairs),
+    // keeping bands at least 2w rows so the ring warm-up stays amortised.
+    const long slots = (long)cu_count() * resident_blocks_per_cu<RAD, NW>();
+    long n_bands = slots / ((long)n_xt * a.batch);
+    if (n_bands < 1) n_bands = 1;
+    int band_rows = (int)((a.H + n_bands - 1) / n_bands);
+    if (band_rows < 2 * WIN) band_rows = 2 * WIN;
     n_bands = (a.H + band_rows - 1) / band_rows;
-    dim3 grid(n_xt, n_bands, a.batch), block(NW * 64);
-    hipLaunchKernelGGL((sad_fast_kernel<RAD, NW, K>), grid, block, 0, s, a.L, a.R, a.disp, a.dist,
-                       a, band_rows);
+    dim3 grid(n_xt, (unsigned)n_bands, a.batch), block(NW * 64);
+    hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a,
+                       band_rows);
     return hipGetLastError();
 }
 
