@@ -84,6 +84,30 @@ def test_ragged_shapes_and_disparity_counts(gpu, seed):
     assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
 
 
+@pytest.mark.parametrize("W", [48, 52, 56, 60, 64, 68, 76, 100, 132, 1916])
+@pytest.mark.parametrize("D,w", [(1, 3), (64, 15), (100, 7), (256, 11)])
+def test_fast_border_tiles(gpu, W, D, w):
+    """Border tiles of the fast kernel: tile 0 replicates column 0, the last
+    tile is aligned to W-16 (overlapping its neighbour when W % 16 != 0), and
+    the tile before it is pulled left when W < 3 tiles' worth of room."""
+    rng = np.random.default_rng(W * 1000 + D + w)
+    H = 37
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    got = gpu_disp(gpu, L, R, D, w, kernel="fast")
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), (W, D, w, _mismatch(got, ref))
+
+
+@pytest.mark.parametrize("W", [4, 44, 46, 50])
+def test_fast_kernel_refuses_narrow_or_ragged(gpu, W):
+    L = torch.zeros((8, W), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.UsvError):
+        StereoBlockMatcher(8, 5, kernel="fast").compute(L, L)
+    # AUTO takes the generic kernel for the same shape
+    assert StereoBlockMatcher(8, 5).compute(L, L).shape == (8, W)
+
+
 @pytest.mark.parametrize("W,H,D,w,metric", [(97, 41, 48, 5, "ssd"), (130, 20, 70, 9, "ssd"),
                                             (64, 33, 17, 21, "sad"), (50, 17, 9, 1, "sad"),
                                             (75, 30, 40, 31, "ssd")])

@@ -26,7 +26,7 @@
 //   * R rows are staged by LDS-DMA (global_load_lds_ubyte writes one u32 per
 //     column) into a per-wave ring of NB row buffers, PD rows ahead, so input
 //     latency is hidden without registers; L rows come through the scalar
-//     cache one row ahead (edge tiles, which clamp, DMA them too).
+//     cache one row ahead, border replication as compile-time byte maps.
 //   * the NW waves' partial minima are combined through LDS every kRB rows.
 // Integer arithmetic only: bit-exact with the oracle by construction.
 #include <type_traits>
@@ -40,7 +40,7 @@ namespace {
 constexpr int kRB = 8;  // output rows buffered between cross-wave combines
 constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_FAST_OCC
-#define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__): 3 -> <= 168 VGPRs
+#define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
 #endif
 
 using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
@@ -65,18 +65,39 @@ struct Cfg {
     static constexpr int NRS = NQ * 64;          // row-buffer stride (entries)
     static constexpr int NB = NW >= 4 ? 4 : 8;   // row buffers per wave
     static constexpr int PD = NB - 1;            // rows in flight ahead of the one computed
-    static constexpr int NPOSP = NPOS <= 32 ? 32 : 64;  // edge-tile L entries per row (pow2)
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - RAD) mod 4, x0 % 4 == 0
-    static constexpr int NLW = (LOFF + NPOS + 3) / 4;  // L dwords (interior tiles): 6 or 8
-    static_assert(NLW == 6 || NLW == 8, "scalar L segment is 6 or 8 dwords");
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
-    static constexpr int LBUF_OFF = RBUF_OFF + NW * NB * NRS;
-    static constexpr int COMB_OFF = LBUF_OFF + NW * NB * NPOSP;
+    static constexpr int COMB_OFF = RBUF_OFF + NW * NB * NRS;
     static constexpr int LUT_OFF = COMB_OFF + 2 * kRB * NW * 64;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
     static_assert(RAD >= 1 && RAD <= 7, "packed-u16 cost needs w <= 15");
-    static_assert(NPOSP <= 64, "one DMA instruction per edge L row");
+};
+
+// Where a tile's L row segment comes from.  Every tile reads its L bytes from
+// one exact-size scalar load; the border replication of the two edge tiles is
+// a compile-time byte map:
+//   kInterior  columns x0-r .. x0+K-1+r, all in range;
+//   kLeft      x0 = 0: load from column 0, positions j < r replicate column 0;
+//   kRight     x0 = W-K (the last tile is aligned to the right border, so it
+//              may overlap its neighbour; both write identical values):
+//              load up to column W-1, the last r positions replicate it.
+enum : int { kInterior = 0, kLeft = 1, kRight = 2 };
+template <int RAD, int EDGE>
+struct LSeg {
+    static constexpr int K = kK, NPOS = K + 2 * RAD;
+    static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - r) mod 4 for x0 % 4 == 0
+    static constexpr int NLD = EDGE == kInterior ? (LOFF + NPOS + 3) / 4
+                             : EDGE == kLeft     ? (K + RAD + 3) / 4
+                                                 : (LOFF + K + RAD) / 4;
+    __device__ static constexpr int base(int x0) { return EDGE == kLeft ? 0 : x0 - RAD - LOFF; }
+    __device__ static constexpr int byte(int j) {
+        return EDGE == kInterior ? LOFF + j
+             : EDGE == kLeft     ? (j < RAD ? 0 : j - RAD)
+                                 : (LOFF + j < LOFF + K + RAD - 1 ? LOFF + j : LOFF + K + RAD - 1);
+    }
+    static_assert(EDGE != kRight || (LOFF + K + RAD) % 4 == 0, "right segment ends on a dword");
+    static_assert(NLD == 5 || NLD == 6 || NLD == 8, "scalar segment is 5, 6 or 8 dwords");
 };
 
 template <int CTRL>
@@ -119,6 +140,14 @@ __device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16], int lane) 
     return min(r4, dpp<kQuadSwap1>(r4));
 }
 
+// k-th vector read of a row in order of first use by the packed chain:
+// interleave the low-half columns [0, HALF) with the high-half ones.
+template <int NV, int HV>
+__device__ __forceinline__ constexpr int read_order(int k) {
+    // first 2*HV reads alternate lo / hi, the rest are the remaining hi columns
+    return k < 2 * HV ? ((k & 1) ? HV + (k >> 1) : (k >> 1)) : k;
+}
+
 template <int VEC> struct VecT;
 template <> struct VecT<1> { using T = uint32_t; };
 template <> struct VecT<2> { using T = uint2; };
@@ -139,6 +168,18 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS-DMA of one byte per lane (zero-extended to a dword at M0 + 4*lane),
+// saddr form: scalar row base + 32-bit lane offset.  Inline asm so the
+// compiler cannot precompute 64-bit per-lane addresses for the look-ahead
+// rows (it hoisted and spilled them); the vmcnt waits are all explicit.
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
+}
+__device__ __forceinline__ void dma_u8(const uint8_t* row, uint32_t voff, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_ubyte %0, %1"
+                 :: "v"(voff), "s"(row), "s"(m0) : "memory", "m0");
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
 // vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
 // stores, so lgkmcnt(0) before the barrier is all the hand-off needs.
@@ -146,59 +187,65 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Scalar-load an exact number of dwords (6 or 8: no read past the row) into SGPRs.
+// Scalar-load an exact number of dwords (5, 6 or 8: never past the row) into SGPRs.
+using su4 = uint32_t __attribute__((ext_vector_type(4)));
+using su2 = uint32_t __attribute__((ext_vector_type(2)));
+using su8 = uint32_t __attribute__((ext_vector_type(8)));
 template <int N> struct SWords;
-template <> struct SWords<6> {
-    struct T { uint32_t __attribute__((ext_vector_type(4))) a; uint32_t __attribute__((ext_vector_type(2))) b; };
-};
-template <> struct SWords<8> {
-    using T = uint32_t __attribute__((ext_vector_type(8)));
-};
+template <> struct SWords<5> { struct T { su4 a; uint32_t b; }; };
+template <> struct SWords<6> { struct T { su4 a; su2 b; }; };
+template <> struct SWords<8> { using T = su8; };
 template <int N>
 __device__ __forceinline__ typename SWords<N>::T s_load_words(const uint8_t* p) {
     typename SWords<N>::T w;
     if constexpr (N == 8) {
         asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(w) : "s"(p) : "memory");
-    } else {
+    } else if constexpr (N == 6) {
         asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx2 %1, %2, 0x10"
+                     : "=s"(w.a), "=s"(w.b) : "s"(p) : "memory");
+    } else {
+        asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dword %1, %2, 0x10"
                      : "=s"(w.a), "=s"(w.b) : "s"(p) : "memory");
     }
     return w;
 }
+// Scalar loads return out of order: only lgkmcnt(0) retires one.  The words
+// are in/out operands so nothing that reads them can be scheduled above.
 template <int N>
 __device__ __forceinline__ void wait_lgkm0(typename SWords<N>::T& w) {
-    if constexpr (N == 8) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w) : : "memory");
-    } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w.a), "+s"(w.b) : : "memory");
-    }
+    if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w) : : "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w.a), "+s"(w.b) : : "memory");
 }
 template <int N>
 __device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uint32_t (&o)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = 0;
     if constexpr (N == 8) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = w[i];
     } else {
-        o[0] = w.a[0]; o[1] = w.a[1]; o[2] = w.a[2]; o[3] = w.a[3];
-        o[4] = w.b[0]; o[5] = w.b[1]; o[6] = 0; o[7] = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = w.a[i];
+        if constexpr (N == 6) { o[4] = w.b[0]; o[5] = w.b[1]; }
+        else o[4] = w.b;
     }
 }
 
-template <int RAD, int NW, bool INTERIOR>
+template <int RAD, int NW, int EDGE>
 __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
                                           const uint8_t* __restrict__ R,
                                           uint8_t* __restrict__ disp, double* __restrict__ dist,
                                           const MatchArgs& a, uint32_t* smem, int lane,
                                           int wave, int x0, int y_begin, int y_end) {
     using C = Cfg<RAD, NW>;
-    using LWords = typename SWords<C::NLW>::T;
+    using LS = LSeg<RAD, EDGE>;
+    using LWords = typename SWords<LS::NLD>::T;
     constexpr int WIN = C::WIN, K = C::K, HALF = C::HALF;
-    constexpr int NDMA = C::NQ + (INTERIOR ? 0 : 1);  // VMEM ops issued per input row
+    constexpr int NDMA = C::NQ;  // VMEM ops issued per input row
     const int l_eff = min(lane, (a.D - 1 - wave) / NW);
     const uint32_t d_eff = (uint32_t)(NW * l_eff + wave);
     const int cbase = x0 - RAD - (NW * 63 + wave);  // first R column this wave stages
     uint32_t* rbuf = smem + C::RBUF_OFF + wave * C::NB * C::NRS;
-    uint32_t* lbuf = smem + C::LBUF_OFF + wave * C::NB * C::NPOSP;
     uint32_t* comb = smem + C::COMB_OFF;
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
@@ -211,39 +258,29 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         return img + (size_t)y * a.pitch;
     };
 
-    // ---- R (and edge-tile L) rows: LDS-DMA into the ring, PD rows ahead ----
+    // ---- R rows: LDS-DMA into the ring, PD rows ahead ----
     // Rows past the band are clamped to real rows: harmless extra loads.
     // Clamped source columns do not depend on the row: 32-bit lane offsets
     // against a scalar row base (the saddr form of the DMA, no 64-bit VGPRs).
     uint32_t colR[C::NQ];
 #pragma unroll
     for (int i = 0; i < C::NQ; ++i) colR[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1);
-    const uint32_t colL = (uint32_t)min(max(x0 - RAD + lane, 0), Wm1);
+    const uint32_t rbase = lds_addr(rbuf);
     auto issue_dma = [&](int t) {
         const int buf = t & (C::NB - 1);
         const uint8_t* rr = row_ptr(R, t);
 #pragma unroll
         for (int i = 0; i < C::NQ; ++i)
-            __builtin_amdgcn_global_load_lds(rr + colR[i], rbuf + buf * C::NRS + 64 * i, 1, 0, 0);
-        if constexpr (!INTERIOR) {
-            const uint8_t* lr = row_ptr(L, t);
-            if (lane < C::NPOSP)
-                __builtin_amdgcn_global_load_lds(lr + colL, lbuf + buf * C::NPOSP, 1, 0, 0);
-        }
+            dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
     };
 
-    // ---- L bytes of the interior path: the row segment through the scalar
-    // cache, requested one row ahead.  Issued as inline asm: the compiler
-    // would otherwise turn it into a vector load (the LDS-DMA intrinsic
-    // defeats its no-clobber proof) and drain the DMA look-ahead with
-    // vmcnt(0).  Scalar loads return out of order, so only lgkmcnt(0) can
-    // retire one; the wait takes the words as operands so nothing that reads
-    // them can be scheduled above it.
+    // ---- L bytes: the row segment through the scalar cache, one row ahead.
+    // Issued as inline asm: the compiler would otherwise turn it into a
+    // vector load (the LDS-DMA intrinsic defeats its no-clobber proof) and
+    // drain the DMA look-ahead with vmcnt(0).
     LWords lw_next;
-    auto load_lw = [&](int t) {
-        const uint8_t* p = row_ptr(L, t) + (x0 - RAD - C::LOFF);
-        lw_next = s_load_words<C::NLW>(p);
-    };
+    auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(row_ptr(L, t) + LS::base(x0)); };
+
     // One input row t: packed chain, H pairs, S / ring update.
     auto do_row = [&](int t, auto warm_tag, auto slot_tag, uint32_t(&S)[HALF],
                       uint32_t(&ring)[WIN][HALF]) {
@@ -255,48 +292,65 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         issue_dma(t + C::PD);
 
         uint32_t Lv[C::NPOS];
-        if constexpr (INTERIOR) {
+        {
             LWords cur = lw_next;
-            wait_lgkm0<C::NLW>(cur);  // row t's words have arrived
-            load_lw(t + 1);   // and row t+1's are requested a full row ahead
+            wait_lgkm0<LS::NLD>(cur);  // row t's words have arrived
             uint32_t lw[8];
-            unpack_words<C::NLW>(cur, lw);
+            unpack_words<LS::NLD>(cur, lw);
 #pragma unroll
             for (int j = 0; j < C::NPOS; ++j) {
-                const int bidx = C::LOFF + j;
+                const int bidx = LS::byte(j);
                 Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
-        } else {
-            // lane j holds clamped column j of the segment; move it to SGPRs
-            const uint32_t lcol = lbuf[buf * C::NPOSP + (lane & (C::NPOSP - 1))];
-#pragma unroll
-            for (int j = 0; j < C::NPOS; ++j) Lv[j] = __builtin_amdgcn_readlane(lcol, j);
         }
 
         using VT = typename VecT<C::VEC>::T;
         const VT* rb = reinterpret_cast<const VT*>(rbuf + buf * C::NRS + s_l);
         uint32_t Rv[C::NPOS_V];
+        // issue the reads in the chain's order of use (step j needs columns j
+        // and j + HALF) so the first steps only wait for the first reads
 #pragma unroll
-        for (int jv = 0; jv < C::NPOS_V / C::VEC; ++jv) {
+        for (int k = 0; k < C::NPOS_V / C::VEC; ++k) {
+            constexpr int NV = C::NPOS_V / C::VEC, HV = HALF / C::VEC;
+            const int jv = read_order<NV, HV>(k);
             const VT v = rb[jv];
 #pragma unroll
             for (int e = 0; e < C::VEC; ++e) Rv[jv * C::VEC + e] = vget<C::VEC>(v, e);
         }
-        // packed prefix: P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)]
-        uint32_t P[C::NSTEP + 1];
-        P[0] = 0;
+        // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)], split
+        // into two independent chains for ILP: A covers steps [0, SP), B
+        // steps [SP, NSTEP) from zero, so P[j] = A[SP] + B[j - SP] for j > SP.
+        constexpr int SP = HALF;
+        constexpr int NB_STEPS = C::NSTEP - SP;
+        uint32_t A[SP + 1], Bc[NB_STEPS + 1];
+        A[0] = 0;
+        Bc[0] = 0;
 #pragma unroll
-        for (int j = 0; j < C::NSTEP; ++j) {
-            P[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
-                                                  __builtin_amdgcn_sad_u8(Lv[j], Rv[j], P[j]));
-            const int x = j + 1 - WIN;  // H pair (x, x + HALF) complete
-            if (x >= 0 && x < HALF) {
-                const uint32_t h = pk_sub(P[x + WIN], P[x]);
-                if constexpr (WARM) S[x] = pk_add(S[x], h);
-                else S[x] = pk_sub(pk_add(S[x], h), ring[SL][x]);
-                ring[SL][x] = h;
+        for (int j = 0; j < (SP > NB_STEPS ? SP : NB_STEPS); ++j) {
+            if (j < SP)
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
+                                                      __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
+            if (j < NB_STEPS) {
+                const int jj = j + SP;
+                Bc[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[jj + HALF], Rv[jj + HALF],
+                                                       __builtin_amdgcn_sad_u8(Lv[jj], Rv[jj], Bc[j]));
             }
         }
+#pragma unroll
+        for (int x = 0; x < HALF; ++x) {
+            // H pair (x, x + HALF) = P[x + WIN] - P[x]
+            uint32_t h;
+            if (x + WIN <= SP) h = pk_sub(A[x + WIN], A[x]);
+            else h = pk_add(Bc[x + WIN - SP], pk_sub(A[SP], A[x]));
+            if constexpr (WARM) S[x] = pk_add(S[x], h);
+            else S[x] = pk_sub(pk_add(S[x], h), ring[SL][x]);
+            ring[SL][x] = h;
+        }
+        // The row's LDS reads are all consumed: request row t+1's L words now,
+        // so the lgkmcnt waits of this row's LDS reads never retire (and wait
+        // for) that scalar load; it has the rest of this row to land.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        load_lw(t + 1);
         // Keep rows apart: interleaving the unrolled warm-up rows only raises
         // register pressure (spills whose reloads would drain the DMA queue).
         __builtin_amdgcn_sched_barrier(0);
@@ -346,7 +400,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // prologue: PD rows in flight, L words of rows 0 and 1 requested
 #pragma unroll
     for (int t = 0; t < C::PD; ++t) issue_dma(t);
-    if constexpr (INTERIOR) load_lw(0);
+    load_lw(0);
 
     using WarmT = std::integral_constant<bool, true>;
     using SteadyT = std::integral_constant<bool, false>;
@@ -369,8 +423,11 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     wait_vmcnt<0>();  // drain the look-ahead DMAs before the wave retires
 }
 
+// r = 7 needs ~175 VGPRs (15-row ring): two waves per SIMD instead of spilling.
+constexpr int fast_occ(int rad) { return rad >= 7 ? 2 : USV_FAST_OCC; }
+
 template <int RAD, int NW>
-__global__ __launch_bounds__(NW * 64, USV_FAST_OCC) void sad_fast_kernel(const uint8_t* __restrict__ L,
+__global__ __launch_bounds__(NW * 64, fast_occ(RAD)) void sad_fast_kernel(const uint8_t* __restrict__ L,
                                                               const uint8_t* __restrict__ R,
                                                               uint8_t* __restrict__ disp,
                                                               double* __restrict__ dist,
@@ -379,7 +436,12 @@ __global__ __launch_bounds__(NW * 64, USV_FAST_OCC) void sad_fast_kernel(const u
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x0 = blockIdx.x * C::K;
+    // x-tile origin: the last tile is aligned to the right border and the one
+    // before it pulled left if needed, so only tiles 0 and n-1 clamp L.
+    const int n_xt = gridDim.x, xt = blockIdx.x;
+    int x0 = xt * C::K;
+    if (xt == n_xt - 1) x0 = a.W - C::K;
+    else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
     const int y_begin = blockIdx.y * band_rows;
     const int y_end = min(a.H, y_begin + band_rows);
     const size_t b = blockIdx.z;
@@ -392,11 +454,12 @@ __global__ __launch_bounds__(NW * 64, USV_FAST_OCC) void sad_fast_kernel(const u
         for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
     }
     __syncthreads();
-    const bool interior = (x0 - RAD >= 0) && (x0 + C::K - 1 + RAD <= a.W - 1);
-    if (interior)
-        band_loop<RAD, NW, true>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    if (xt == 0)
+        band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    else if (xt == n_xt - 1)
+        band_loop<RAD, NW, kRight>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
     else
-        band_loop<RAD, NW, false>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+        band_loop<RAD, NW, kInterior>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
 }
 
 // Blocks resident per CU for this instantiation (queried once).
@@ -451,8 +514,9 @@ hipError_t launch_r(const MatchArgs& a, hipStream_t s) {
 }  // namespace
 
 bool fast_path_supported(const MatchArgs& a) {
+    // W % 4 == 0 and W >= 3 tiles: the border tiles' L maps are compile-time
     return a.metric == 0 && a.w >= 3 && a.w <= 15 && (a.w & 1) && a.D >= 1 && a.D <= 256 &&
-           (a.pitch % 4) == 0 && (reinterpret_cast<uintptr_t>(a.L) % 4) == 0 &&
+           (a.W % 4) == 0 && a.W >= 3 * kK && (a.pitch % 4) == 0 && (reinterpret_cast<uintptr_t>(a.L) % 4) == 0 &&
            (reinterpret_cast<uintptr_t>(a.R) % 4) == 0 && (a.batch <= 1 || a.pair_stride % 4 == 0);
 }
 
