@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build an A/B variant of libusv.so with extra defines for the fast kernel:
+#   scripts/build_variant.sh <name> -DUSV_XCD_REMAP=0 ...
+# -> build_variants/<name>.so (same C ABI; select with USV_LIB_PATH).
+set -e
+cd "$(dirname "$0")/.."
+name=$1; shift
+C=unsynchronized_stereo_vision_proj325_amd/csrc
+make -s -C $C
+mkdir -p build_variants
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -ffp-contract=off "$@" \
+    -c $C/usv_sad_fast.hip -o build_variants/$name.fast.o
+objs=$(ls $C/build/*.o | grep -v usv_sad_fast.o)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.fast.o $objs
+rm -f build_variants/$name.fast.o
+echo built build_variants/$name.so

@@ -8,7 +8,7 @@ fatal() { case "$1" in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && ret
 step() { local name=$1 to=$2; shift 2; echo "=== $name ($(date +%T))"
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
   echo "=== $name rc=$rc"; tail -n 6 "gpurun_out/$name.log"
-  if fatal $rc; then echo "FATAL rc=$rc in $name"; exit $rc; fi; return $rc; }
+  if fatal $rc || [ $rc -ne 0 ]; then echo "FAILED rc=$rc in $name: stopping"; exit $rc; fi; return $rc; }
 [ -x scripts/probes/glds_probe ] && step probe 60 scripts/probes/glds_probe
 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 step bench_default 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline

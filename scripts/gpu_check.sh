@@ -11,7 +11,9 @@ step() {  # step <name> <timeout> <cmd...>
   local rc=$?
   echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
-  return $rc
+  # any failure may be a GPU fault: start nothing more on the GPU in this call
+  if [ $rc -ne 0 ]; then echo "FAILED rc=$rc in $name: stopping"; exit $rc; fi
+  return 0
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider

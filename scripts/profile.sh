@@ -16,7 +16,7 @@ run() {  # run <name> <rocprofv3 args...>
      > $OUT/$name.log 2>&1
   local rc=$?
   echo "=== $name rc=$rc"; tail -n 3 $OUT/$name.log
-  if fatal $rc; then echo "FATAL rc=$rc in $name"; exit $rc; fi
+  if fatal $rc || [ $rc -ne 0 ]; then echo "FAILED rc=$rc in $name: stopping"; exit $rc; fi
 }
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 run trace --kernel-trace --stats

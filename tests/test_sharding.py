@@ -44,12 +44,18 @@ def _worker(rank, world, port, batch, q):
             torch.empty((0, 6, 10), dtype=torch.uint8)
         out = gather_disparity(local, batch)
         pend = gather_disparity(local, batch, async_op=True).wait()
+        width = max(pair_range(batch, r, world)[1] - pair_range(batch, r, world)[0] for r in range(world))
+        recv = [torch.empty((width, 6, 10), dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
+        parts = gather_disparity(local, batch, recv=recv, concat=False)
+        if rank == 0:
+            parts = torch.cat(parts, 0)
         if rank == 0:
             exp = torch.stack([(torch.arange(60, dtype=torch.int32).reshape(6, 10) + 7 * i) % 256
                                for i in range(batch)]).to(torch.uint8)
-            q.put(("ok", bool(torch.equal(out, exp)) and bool(torch.equal(pend, exp))))
+            q.put(("ok", bool(torch.equal(out, exp)) and bool(torch.equal(pend, exp))
+                   and bool(torch.equal(parts, exp))))
         else:
-            q.put(("none", out is None and pend is None))
+            q.put(("none", out is None and pend is None and parts is None))
     finally:
         dist.destroy_process_group()
 

@@ -39,6 +39,9 @@ namespace {
 
 constexpr int kRB = 8;  // output rows buffered between cross-wave combines
 constexpr int kK = 16;  // outputs per x-tile
+#ifndef USV_XCD_REMAP
+#define USV_XCD_REMAP 1  // XCD-contiguous tile order (0: plain linear order, for A/B runs)
+#endif
 #ifndef USV_FAST_OCC
 #define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
 #endif
@@ -188,6 +191,8 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // Scalar-load an exact number of dwords (5, 6 or 8: never past the row) into SGPRs.
+// Two-instruction forms use early-clobber outputs: the first load's
+// destination must not overlap the base the second one reads.
 using su4 = uint32_t __attribute__((ext_vector_type(4)));
 using su2 = uint32_t __attribute__((ext_vector_type(2)));
 using su8 = uint32_t __attribute__((ext_vector_type(8)));
@@ -202,10 +207,10 @@ __device__ __forceinline__ typename SWords<N>::T s_load_words(const uint8_t* p) 
         asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(w) : "s"(p) : "memory");
     } else if constexpr (N == 6) {
         asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx2 %1, %2, 0x10"
-                     : "=s"(w.a), "=s"(w.b) : "s"(p) : "memory");
+                     : "=&s"(w.a), "=&s"(w.b) : "s"(p) : "memory");
     } else {
         asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dword %1, %2, 0x10"
-                     : "=s"(w.a), "=s"(w.b) : "s"(p) : "memory");
+                     : "=&s"(w.a), "=&s"(w.b) : "s"(p) : "memory");
     }
     return w;
 }
@@ -431,20 +436,34 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD)) void sad_fast_kernel(const 
                                                               const uint8_t* __restrict__ R,
                                                               uint8_t* __restrict__ disp,
                                                               double* __restrict__ dist,
-                                                              MatchArgs a, int band_rows) {
+                                                              MatchArgs a, int band_rows, int n_xt,
+                                                              int n_bands) {
     using C = Cfg<RAD, NW>;
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware tile order.  Workgroups are dispatched round-robin over the 8
+    // XCDs (linear id mod 8), each with its own L2: renumber so XCD k owns the
+    // k-th contiguous run of (x-tile, band, pair) in x-fastest order.  Tiles of
+    // one band then share an L2 and every R/L row is fetched from HBM about
+    // once instead of once per XCD.  A bijection whatever the real placement.
+    const unsigned total = gridDim.x, lin = blockIdx.x;
+    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
+#if USV_XCD_REMAP
+    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
+#else
+    const unsigned tile = lin + 0u * (xcd + base + rem);
+#endif
+    const int xt = (int)(tile % (unsigned)n_xt);
+    const int band = (int)((tile / (unsigned)n_xt) % (unsigned)n_bands);
+    const size_t b = tile / ((unsigned)n_xt * (unsigned)n_bands);
     // x-tile origin: the last tile is aligned to the right border and the one
     // before it pulled left if needed, so only tiles 0 and n-1 clamp L.
-    const int n_xt = gridDim.x, xt = blockIdx.x;
     int x0 = xt * C::K;
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
-    const int y_begin = blockIdx.y * band_rows;
+    const int y_begin = band * band_rows;
     const int y_end = min(a.H, y_begin + band_rows);
-    const size_t b = blockIdx.z;
     L += b * a.pair_stride;
     R += b * a.pair_stride;
     disp += b * a.disp_stride;
@@ -498,9 +517,11 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     int band_rows = (int)((a.H + n_bands - 1) / n_bands);
     if (band_rows < 2 * WIN) band_rows = 2 * WIN;
     n_bands = (a.H + band_rows - 1) / band_rows;
-    dim3 grid(n_xt, (unsigned)n_bands, a.batch), block(NW * 64);
+    const long total = (long)n_xt * n_bands * a.batch;
+    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a,
-                       band_rows);
+                       band_rows, n_xt, (int)n_bands);
     return hipGetLastError();
 }
 

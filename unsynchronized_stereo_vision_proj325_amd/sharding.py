@@ -22,12 +22,16 @@ def pair_range(batch: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
-def gather_disparity(local: torch.Tensor, batch: int, dst: int = 0, group=None, async_op: bool = False):
+def gather_disparity(local: torch.Tensor, batch: int, dst: int = 0, group=None, async_op: bool = False,
+                     recv: list | None = None, concat: bool = True):
     """Gather every rank's (n_local, H, W) u8 maps into a (batch, H, W) tensor on `dst`.
 
     Shards may be uneven; each rank pads to the largest shard so one gather
-    call moves everything.  Returns (result_or_None, work) when async_op, else
-    result_or_None (the tensor on dst, None elsewhere).
+    call moves everything.  `recv` (dst only): reusable receive buffers, one
+    (max_shard, H, W) tensor per rank (a steady-state loop allocates nothing).
+    `concat=False` returns the per-rank shards as a list of views instead of
+    copying them into one tensor.  Returns the result on dst (None elsewhere),
+    or, with async_op, a handle whose wait() returns it.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -40,7 +44,11 @@ def gather_disparity(local: torch.Tensor, batch: int, dst: int = 0, group=None, 
         pad = torch.zeros((width - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                           device=local.device)
         send = torch.cat([local, pad], 0)
-    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    bufs = None
+    if rank == dst:
+        bufs = recv if recv is not None else [torch.empty_like(send) for _ in range(world)]
+        if len(bufs) != world or any(b.shape != send.shape or b.dtype != send.dtype for b in bufs):
+            raise ValueError("recv must hold one buffer per rank shaped like the padded shard")
     work = dist.gather(send.contiguous(), bufs, dst=dst, group=group, async_op=async_op)
 
     def assemble():
@@ -50,7 +58,7 @@ def gather_disparity(local: torch.Tensor, batch: int, dst: int = 0, group=None, 
         for r in range(world):
             s, e = pair_range(batch, r, world)
             parts.append(bufs[r][: e - s])
-        return torch.cat(parts, 0)
+        return torch.cat(parts, 0) if concat else parts
 
     if async_op:
         class _Pending:
