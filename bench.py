@@ -32,8 +32,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from unsynchronized_stereo_vision_proj325_amd import StereoBlockMatcher  # noqa: E402
+from unsynchronized_stereo_vision_proj325_amd.sharding import gather_disparity, pair_range  # noqa: E402
 from unsynchronized_stereo_vision_proj325_amd.synthetic import synthetic_pair  # noqa: E402
 
+# BASELINE.json's metric, verbatim (value = disparity-pixels/s; achieved HBM GB/s is roofline.achieved)
+BASELINE_METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (32-bit VALU, MI355X_MICROARCH.md)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
@@ -55,19 +58,25 @@ def parse():
     return p.parse_args()
 
 
-def traffic_from_profiles(workload_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one exists for this workload."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+def profile_counters(workload_key: str):
+    """Per-launch counters of the committed rocprofv3 run for this workload
+    (profiles/counters.json, written by scripts/summarize_profile.py), or None."""
+    path = os.path.join(ROOT, "profiles", "counters.json")
     if not os.path.exists(path):
-        return None, None
+        return None
     try:
-        d = json.load(open(path))
-        e = d.get(workload_key)
-        if e:
-            return float(e["bytes_per_launch"]), e.get("source")
-    except Exception:
-        pass
-    return None, None
+        return json.load(open(path)).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def fast_kernel_name(W: int, D: int, w: int, pitch: int) -> str:
+    """Which kernel the AUTO dispatch takes for this shape (csrc/usv_sad_fast.hip
+    fast_path_supported / launch_r), for labelling the roofline entry."""
+    if 3 <= w <= 15 and w % 2 == 1 and 1 <= D <= 256 and W % 4 == 0 and W >= 48 and pitch % 4 == 0:
+        nw = 1 if D <= 64 else (2 if D <= 128 else 4)
+        return f"sad_fast_kernel<{(w - 1) // 2}, {nw}>"
+    return "sad_generic_kernel"
 
 
 def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float):
@@ -117,18 +126,20 @@ def main():
 
     W, H, D, w = a.width, a.height, a.disparities, a.window
     with_dist = not a.no_distance
-    # rank r owns pair r (weak scaling: one pair per rank per step)
-    L, R, _ = synthetic_pair(W, H, D, pair_index=rank, noise=2)
+    # weak scaling: a batch of `world` independent pairs, pair i -> rank i (sharding.pair_range)
+    first, stop = pair_range(world, rank, world)
+    assert stop - first == 1
+    L, R, _ = synthetic_pair(W, H, D, pair_index=first, noise=2)
     Lt = torch.from_numpy(L).to(dev)
     Rt = torch.from_numpy(R).to(dev)
     matcher = StereoBlockMatcher(D, w)
     nbuf = 2
-    disp_bufs = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    disp_bufs = [torch.empty((1, H, W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     dist_bufs = [torch.empty((H, W), dtype=torch.float64, device=dev) for _ in range(nbuf)] if with_dist else None
-    gather_lists = None
+    recv = None
     if world > 1 and rank == 0 and a.gather != "none":
-        gather_lists = [[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(world)]
-                        for _ in range(nbuf)]
+        recv = [[torch.empty((1, H, W), dtype=torch.uint8, device=dev) for _ in range(world)]
+                for _ in range(nbuf)]
     stream = torch.cuda.current_stream()
     pending = [None] * nbuf
 
@@ -139,13 +150,14 @@ def main():
             pending[b] = None
         if ev_pair is not None:
             ev_pair[0].record(stream)
-        matcher.compute(Lt, Rt, with_distance=with_dist, out_disp=disp_bufs[b],
+        matcher.compute(Lt, Rt, with_distance=with_dist, out_disp=disp_bufs[b][0],
                         out_dist=dist_bufs[b] if with_dist else None)
         if ev_pair is not None:
             ev_pair[1].record(stream)
         if world > 1 and a.gather != "none":
-            work = dist.gather(disp_bufs[b], gather_lists[b] if rank == 0 else None, dst=0,
-                               async_op=True)
+            # rank 0 collects every rank's u8 map over RCCL (xGMI); no concat copy
+            work = gather_disparity(disp_bufs[b], world, dst=0, async_op=True,
+                                    recv=recv[b] if rank == 0 else None, concat=False)
             if a.gather == "sync":
                 work.wait()
             else:
@@ -187,11 +199,10 @@ def main():
     alg_bytes = bytes_per_px * pixels
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload_key = f"C_{W}x{H}_w{w}_D{D}_{'dist' if with_dist else 'nodist'}"
-    traffic, traffic_src = traffic_from_profiles(workload_key)
-    # sliding-window VALU work of the fast kernel: ~7.3 lane-ops per (pixel, disparity)
-    valu_ops = 7.3 * pixels * D
+    prof = profile_counters(workload_key)
+    kname = fast_kernel_name(W, D, w, W)
     rec = {
-        "metric": "disparity-pixels/s (1920x1080, 11x11 SAD, 128 disparities)",
+        "metric": BASELINE_METRIC,
         "value": value,
         "unit": "disparity-pixels/s",
         "n_gpus": world,
@@ -218,19 +229,24 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
+            "traffic": prof.get("bytes_per_launch") if prof else None,
+            "traffic_source": prof.get("source") if prof else None,
             "algorithmic_bytes_per_launch": alg_bytes,
-            "kernel": "sad_fast_kernel<5,2,16>",
-            "note": "fused kernel is VALU-integer bound (SURVEY.md 8(d)); see valu_roofline",
-        },
-        "valu_roofline": {
-            "achieved_lane_ops_per_s": valu_ops / (kern_ms * 1e-3),
-            "peak": VALU_PEAK_LANE_OPS,
-            "frac": valu_ops / (kern_ms * 1e-3) / VALU_PEAK_LANE_OPS,
-            "ops_model": "7.3 VALU lane-ops per (pixel, disparity), counted from the kernel ISA",
+            "kernel": kname,
+            "kernel_avg_us_rocprof": prof["avg_ns"] / 1e3 if prof else None,
+            "note": "HBM is not the binding roof: the fused kernel is VALU-integer bound "
+                    "(SURVEY.md 8(d)); see valu_roofline",
         },
     }
+    if prof and prof.get("valu_insts_per_launch"):
+        lane_ops = prof["valu_insts_per_launch"] * 64  # wave64 VALU instructions -> lane-ops
+        rec["valu_roofline"] = {
+            "achieved_lane_ops_per_s": lane_ops / (kern_ms * 1e-3),
+            "peak": VALU_PEAK_LANE_OPS,
+            "frac": lane_ops / (kern_ms * 1e-3) / VALU_PEAK_LANE_OPS,
+            "lane_ops_per_element": lane_ops / (pixels * D),
+            "source": "SQ_INSTS_VALU per launch x 64 from profiles/counters.json, over this run's kernel time",
+        }
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
         rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]
