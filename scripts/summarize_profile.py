@@ -6,8 +6,12 @@ profiles/counters.json that bench.py reads for roofline.traffic.
     python scripts/summarize_profile.py <tag> [--workload KEY] [--kernel SUBSTR]
 
 HBM traffic per launch follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
-WRITE_SIZE come from separate --pmc passes, are in KiB, and FETCH_SIZE is
-doubled on gfx950 (it tallies 128-B requests at 64 B).
+WRITE_SIZE come from separate --pmc passes and are in KiB.  The guide's x2
+FETCH correction is calibrated for 16-B/lane streaming reads; for other access
+widths it says to calibrate on a known byte count.  This kernel reads with
+1-B LDS-DMA and scalar loads, and --fetch-factor records the calibration used
+(see profiles/README.md: raw FETCH_SIZE equals the compulsory L+R bytes, and
+the x2 reading of the no-remap build exceeds the 8-XCD upper bound).
 """
 from __future__ import annotations
 
@@ -49,6 +53,8 @@ def main():
     ap.add_argument("--workload", default="C_1920x1080_w11_D128_dist")
     ap.add_argument("--kernel", default="sad_fast_kernel")
     ap.add_argument("--src", default=None, help="default gpurun_out/prof_<tag>")
+    ap.add_argument("--fetch-factor", type=float, default=1.0,
+                    help="FETCH_SIZE calibration (guide: 2 for 16-B/lane streaming reads)")
     a = ap.parse_args()
     src = a.src or os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     dst = os.path.join(ROOT, "profiles", a.tag)
@@ -70,7 +76,7 @@ def main():
                 shutil.copy(next(os.path.join(d, f) for f in os.listdir(d) if f.endswith("counter_collection.csv")),
                             os.path.join(dst, f"{p}.csv"))
 
-    fetch_b = c.get("FETCH_SIZE", 0.0) * 1024 * 2  # KiB, x2 gfx950 correction
+    fetch_b = c.get("FETCH_SIZE", 0.0) * 1024 * a.fetch_factor  # KiB -> B, calibrated
     write_b = c.get("WRITE_SIZE", 0.0) * 1024
     hbm = fetch_b + write_b if "FETCH_SIZE" in c and "WRITE_SIZE" in c else None
     entry = {
@@ -78,12 +84,14 @@ def main():
         "avg_ns": avg_ns,
         "calls": int(dom["Calls"]),
         "fetch_bytes_per_launch": fetch_b if "FETCH_SIZE" in c else None,
+        "fetch_size_kib_raw": c.get("FETCH_SIZE"),
+        "fetch_factor": a.fetch_factor,
         "write_bytes_per_launch": write_b if "WRITE_SIZE" in c else None,
         "bytes_per_launch": hbm,
         "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
         "counters": c,
         "source": f"profiles/{a.tag}/ (rocprofv3 --kernel-trace --stats; separate --pmc passes; "
-                  "FETCH_SIZE KiB x2 per MI355X_MICROARCH.md HBM note)",
+                  f"bytes = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE, KiB x 1024)",
     }
     table = os.path.join(ROOT, "profiles", "counters.json")
     allc = json.load(open(table)) if os.path.exists(table) else {}
@@ -100,7 +108,7 @@ def main():
     for k in sorted(c):
         lines.append(f"| {k} | {c[k]:.6g} |")
     if hbm is not None:
-        lines += ["", f"HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE = {hbm/1e6:.2f} MB "
+        lines += ["", f"HBM bytes per launch = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE = {hbm/1e6:.2f} MB "
                       f"({hbm / (avg_ns * 1e-9) / 1e9:.0f} GB/s over the {avg_ns/1e3:.1f} µs average)"]
     if c.get("SQ_INSTS_VALU"):
         lane_ops = c["SQ_INSTS_VALU"] * 64

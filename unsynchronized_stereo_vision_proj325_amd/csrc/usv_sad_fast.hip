@@ -37,22 +37,28 @@
 namespace usv {
 namespace {
 
-constexpr int kRB = 8;  // output rows buffered between cross-wave combines
+#ifndef USV_KRB
+#define USV_KRB 8
+#endif
+constexpr int kRB = USV_KRB;  // output rows buffered between cross-wave combines
 constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_XCD_REMAP
 #define USV_XCD_REMAP 1  // XCD-contiguous tile order (0: plain linear order, for A/B runs)
 #endif
+#ifndef USV_STAMPS
+#define USV_STAMPS 0  // diagnostic build: per-phase s_memtime totals (scripts/stamps.py)
+#endif
+// Timing experiments only (wrong results): USV_EXP=1 no R DMA, 2 no flush
+// barrier, 3 trivial reduction.  Never set in the product build.
+#ifndef USV_EXP
+#define USV_EXP 0
+#endif
+#ifndef USV_SPLIT_CHAIN
+#define USV_SPLIT_CHAIN 1  // two independent prefix chains per row (ILP); 0: one chain
+#endif
 #ifndef USV_FAST_OCC
 #define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
 #endif
-
-using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
-}
-__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
-}
 
 template <int RAD, int NW>
 struct Cfg {
@@ -72,7 +78,7 @@ struct Cfg {
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
     static constexpr int COMB_OFF = RBUF_OFF + NW * NB * NRS;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * kRB * NW * 64;
+    static constexpr int LUT_OFF = COMB_OFF + 2 * kRB * NW * K;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
     static_assert(RAD >= 1 && RAD <= 7, "packed-u16 cost needs w <= 15");
 };
@@ -112,20 +118,14 @@ constexpr int kRowHalfMirror = 0x141;
 constexpr int kQuadSwap2 = 0x4E;  // quad_perm [2,3,0,1]
 constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]
 
-// One transposing round inside 16-lane rows: lanes of the low half (by the
-// round's bit) keep a's pixel, the high half b's; each takes the min with its
-// mirror partner in the other half.
-template <int CTRL>
-__device__ __forceinline__ uint32_t tr_round(uint32_t a, uint32_t b, bool hi) {
-    const uint32_t u = hi ? b : a;
-    const uint32_t v = hi ? a : b;
-    return min(u, dpp<CTRL>(v));
-}
-
-// 16 keys (64-lane vectors over disparities) -> lane l holds the min key of pixel l >> 2.
-__device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16], int lane) {
-    const bool h8 = lane & 8, h4 = lane & 4;
-    uint32_t r1[8], r2[4], r3[2];
+// 16 keys (64-lane vectors over disparities) -> every lane of 16-lane row q
+// holds the min keys of pixels 4q .. 4q+3 in out[0..3].
+// Two transposing swaps (lanes l, l^32 then l, l^16) halve the key count per
+// round; the last 4 keys are then min-all-reduced inside each row by four DPP
+// rounds (mirror, half-mirror, quad xor 2, quad xor 1: every lane meets all
+// 16), which needs no per-lane selects (v_cndmask is ~4x a VALU slot here).
+__device__ __forceinline__ void reduce16(const uint32_t (&k)[16], uint32_t (&out)[4]) {
+    uint32_t r1[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         auto p = __builtin_amdgcn_permlane32_swap(k[i], k[i + 8], false, false);
@@ -134,13 +134,16 @@ __device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16], int lane) 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         auto p = __builtin_amdgcn_permlane16_swap(r1[i], r1[i + 4], false, false);
-        r2[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 4q
+        out[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 4q
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) r3[i] = tr_round<kRowMirror>(r2[i], r2[i + 2], h8);
-    uint32_t r4 = tr_round<kRowHalfMirror>(r3[0], r3[1], h4);
-    r4 = min(r4, dpp<kQuadSwap2>(r4));
-    return min(r4, dpp<kQuadSwap1>(r4));
+    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kRowMirror>(out[i]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kRowHalfMirror>(out[i]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kQuadSwap2>(out[i]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kQuadSwap1>(out[i]));
 }
 
 // k-th vector read of a row in order of first use by the packed chain:
@@ -236,6 +239,28 @@ __device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uin
     }
 }
 
+#if USV_STAMPS
+// phases: 0 DMA wait, 1 L-word wait, 2 chain+H+S, 3 keys+reduce, 4 flush, 5 rows, 6 waves, 7 total
+__device__ unsigned long long g_usv_stamps[8];
+struct Stamps {
+    uint64_t acc[5] = {0, 0, 0, 0, 0}, last = 0, t_begin = 0, rows = 0;
+    __device__ static uint64_t now() {
+        uint64_t t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    }
+    __device__ void mark(int phase) { const uint64_t t = now(); acc[phase] += t - last; last = t; }
+    __device__ void skip() { last = now(); }
+};
+#define USV_STAMP(p) st.mark(p)
+#define USV_STAMP_SKIP() st.skip()
+#else
+#define USV_STAMP(p) ((void)0)
+#define USV_STAMP_SKIP() ((void)0)
+#endif
+
 template <int RAD, int NW, int EDGE>
 __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
                                           const uint8_t* __restrict__ R,
@@ -276,7 +301,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         const uint8_t* rr = row_ptr(R, t);
 #pragma unroll
         for (int i = 0; i < C::NQ; ++i)
-            dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
+            if (USV_EXP != 1) dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
     };
 
     // ---- L bytes: the row segment through the scalar cache, one row ahead.
@@ -287,6 +312,10 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(row_ptr(L, t) + LS::base(x0)); };
 
     // One input row t: packed chain, H pairs, S / ring update.
+#if USV_STAMPS
+    Stamps st;
+    st.t_begin = st.last = Stamps::now();
+#endif
     auto do_row = [&](int t, auto warm_tag, auto slot_tag, uint32_t(&S)[HALF],
                       uint32_t(&ring)[WIN][HALF]) {
         constexpr bool WARM = decltype(warm_tag)::value;
@@ -295,11 +324,13 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         wait_vmcnt<(C::PD - 1) * NDMA>();  // row t has landed in LDS
         __builtin_amdgcn_wave_barrier();
         issue_dma(t + C::PD);
+        USV_STAMP(0);
 
         uint32_t Lv[C::NPOS];
         {
             LWords cur = lw_next;
             wait_lgkm0<LS::NLD>(cur);  // row t's words have arrived
+            USV_STAMP(1);
             uint32_t lw[8];
             unpack_words<LS::NLD>(cur, lw);
 #pragma unroll
@@ -325,7 +356,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)], split
         // into two independent chains for ILP: A covers steps [0, SP), B
         // steps [SP, NSTEP) from zero, so P[j] = A[SP] + B[j - SP] for j > SP.
-        constexpr int SP = HALF;
+        constexpr int SP = USV_SPLIT_CHAIN ? HALF : C::NSTEP;  // 0: one serial chain (B empty)
         constexpr int NB_STEPS = C::NSTEP - SP;
         uint32_t A[SP + 1], Bc[NB_STEPS + 1];
         A[0] = 0;
@@ -345,16 +376,25 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         for (int x = 0; x < HALF; ++x) {
             // H pair (x, x + HALF) = P[x + WIN] - P[x]
             uint32_t h;
-            if (x + WIN <= SP) h = pk_sub(A[x + WIN], A[x]);
-            else h = pk_add(Bc[x + WIN - SP], pk_sub(A[SP], A[x]));
-            if constexpr (WARM) S[x] = pk_add(S[x], h);
-            else S[x] = pk_sub(pk_add(S[x], h), ring[SL][x]);
+            // Packed pairs, but every intermediate half stays in [0, 65535]
+            // (prefixes are monotone, S - ring is a w-1 row sum), so plain
+            // 32-bit add/sub give the packed result exactly: v_add/v_sub_u32
+            // issue at full rate, v_pk_*_u16 at half rate on gfx950
+            // (scripts/probes/valu_rate.hip).
+            if (x + WIN <= SP) h = A[x + WIN] - A[x];
+            else h = Bc[x + WIN - SP] + (A[SP] - A[x]);
+            if constexpr (WARM) S[x] = S[x] + h;
+            else S[x] = (S[x] - ring[SL][x]) + h;
             ring[SL][x] = h;
         }
         // The row's LDS reads are all consumed: request row t+1's L words now,
         // so the lgkmcnt waits of this row's LDS reads never retire (and wait
         // for) that scalar load; it has the rest of this row to land.
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        USV_STAMP(2);
+#if USV_STAMPS
+        st.rows++;
+#endif
         load_lw(t + 1);
         // Keep rows apart: interleaving the unrolled warm-up rows only raises
         // register pressure (spills whose reloads would drain the DMA queue).
@@ -364,14 +404,13 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // ---- output: per-row keys -> LDS, cross-wave min every kRB rows ----
     int slot = 0, cb = 0, y_chunk = y_begin;
     auto flush = [&]() {
-        lds_barrier();
+        if (USV_EXP != 2) lds_barrier();
         const int items = slot * K;
         for (int i = threadIdx.x; i < items; i += NW * 64) {
             const int row = i / K, p = i - row * K;
             uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2)
-                key = min(key, comb[((cb * kRB + row) * NW + w2) * 64 + p * (64 / K)]);
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * kRB + row) * NW + w2) * K + p]);
             const int x = x0 + p;
             if (x < a.W) {
                 const uint32_t dv = key & 0xFFu;
@@ -391,10 +430,23 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             keys[i] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c050400u);         // (S.lo << 8) | d
             keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
         }
-        const uint32_t m = reduce16(keys, lane);
-        comb[((cb * kRB + slot) * NW + wave) * 64 + lane] = m;
+        uint32_t m[4];
+        if constexpr (USV_EXP == 3) {
+            m[0] = m[1] = m[2] = m[3] = keys[0];
+#pragma unroll
+            for (int i = 1; i < K; ++i) m[i & 3] ^= keys[i];
+        } else {
+            reduce16(keys, m);
+        }
+        if ((lane & 15) == 0)  // one lane per 16-lane row stores its 4 pixels
+            *reinterpret_cast<uint4*>(comb + ((cb * kRB + slot) * NW + wave) * K + (lane >> 2)) =
+                make_uint4(m[0], m[1], m[2], m[3]);
         ++slot;
-        if (slot == kRB || last) flush();
+        USV_STAMP(3);
+        if (slot == kRB || last) {
+            flush();
+            USV_STAMP(4);
+        }
     };
 
     uint32_t S[HALF];
@@ -426,13 +478,22 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         }(std::make_integer_sequence<int, WIN>{});
     }
     wait_vmcnt<0>();  // drain the look-ahead DMAs before the wave retires
+#if USV_STAMPS
+    if (lane == 0) {
+        for (int i = 0; i < 5; ++i) atomicAdd(&g_usv_stamps[i], (unsigned long long)st.acc[i]);
+        atomicAdd(&g_usv_stamps[5], (unsigned long long)st.rows);
+        atomicAdd(&g_usv_stamps[6], 1ull);
+        atomicAdd(&g_usv_stamps[7], (unsigned long long)(Stamps::now() - st.t_begin));
+    }
+#endif
 }
 
-// r = 7 needs ~175 VGPRs (15-row ring): two waves per SIMD instead of spilling.
-constexpr int fast_occ(int rad) { return rad >= 7 ? 2 : USV_FAST_OCC; }
+// r = 7 (15-row ring) and r = 6 with four waves need more than 168 VGPRs:
+// two waves per SIMD instead of spilling (tests/test_isa_lint.py checks).
+constexpr int fast_occ(int rad, int nw) { return (rad >= 7 || (rad == 6 && nw == 4)) ? 2 : USV_FAST_OCC; }
 
 template <int RAD, int NW>
-__global__ __launch_bounds__(NW * 64, fast_occ(RAD)) void sad_fast_kernel(const uint8_t* __restrict__ L,
+__global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(const uint8_t* __restrict__ L,
                                                               const uint8_t* __restrict__ R,
                                                               uint8_t* __restrict__ disp,
                                                               double* __restrict__ dist,
@@ -533,6 +594,17 @@ hipError_t launch_r(const MatchArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+#if USV_STAMPS
+extern "C" __attribute__((visibility("default"))) int usv_debug_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_usv_stamps), sizeof(g_usv_stamps)) != hipSuccess) return 1;
+    if (reset) {
+        static const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_usv_stamps), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 bool fast_path_supported(const MatchArgs& a) {
     // W % 4 == 0 and W >= 3 tiles: the border tiles' L maps are compile-time
