@@ -53,6 +53,53 @@ PROBE(p_bfe_u32, "v_bfe_u32 %0, %1, 8, 8")
 PROBE(p_max3_u32, "v_max3_u32 %0, %1, %2, %0")
 PROBE(p_pk_mad_u16, "v_pk_mad_u16 %0, %1, %2, %0")
 
+// Mixed streams: cycles per loop iteration (16 VALU [+ 16 or 8 SALU]) per SIMD.
+#define SBODY8                                                                          \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s0) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s1) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s2) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s3) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s4) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s5) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s6) : "s"(sb) : "scc");                \
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(s7) : "s"(sb) : "scc");
+#define MIXPROBE(NAME, BODY)                                                            \
+    __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint64_t* cyc) {        \
+        uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, \
+                 a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                \
+        uint32_t b = threadIdx.x * 3u + 1u, c = threadIdx.x ^ 0x55u;                    \
+        uint32_t s0 = blockIdx.x, s1 = s0 + 1, s2 = s0 + 2, s3 = s0 + 3, s4 = s0 + 4,  \
+                 s5 = s0 + 5, s6 = s0 + 6, s7 = s0 + 7, sb = blockIdx.x * 7 + 1;        \
+        uint64_t t0 = __builtin_amdgcn_s_memtime();                                     \
+        for (int i = 0; i < ITER; ++i) { BODY }                                         \
+        uint64_t t1 = __builtin_amdgcn_s_memtime();                                     \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 \
+            ^ s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7;                                    \
+        if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0; \
+    }
+// VALU with an SGPR source operand, cndmask with a real mask, DPP move
+#define SBODY_V8(INSN)                                                                  \
+    asm volatile(INSN : "+v"(a0) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a1) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a2) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a3) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a4) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a5) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a6) : "s"(sb), "v"(c));                                    \
+    asm volatile(INSN : "+v"(a7) : "s"(sb), "v"(c));
+MIXPROBE(m_sad_sgpr, SBODY_V8("v_sad_u8 %0, %1, %2, %0") SBODY_V8("v_sad_u8 %0, %1, %2, %0"))
+MIXPROBE(m_cnd_mask, asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(b), "v"(c) : "vcc");
+         BODY8("v_cndmask_b32 %0, %1, %0, vcc") BODY8("v_cndmask_b32 %0, %1, %0, vcc"))
+MIXPROBE(m_cnd_e64, asm volatile("v_cmp_gt_u32 s[40:41], %0, %1" :: "v"(b), "v"(c) : "s40", "s41");
+         BODY8("v_cndmask_b32_e64 %0, %1, %0, s[40:41]") BODY8("v_cndmask_b32_e64 %0, %1, %0, s[40:41]"))
+MIXPROBE(m_mov_dpp, BODY8("v_mov_b32_dpp %0, %1 row_mirror row_mask:0xf bank_mask:0xf")
+         BODY8("v_mov_b32_dpp %0, %1 row_mirror row_mask:0xf bank_mask:0xf"))
+MIXPROBE(m_valu16, BODY8("v_sad_u8 %0, %1, %2, %0") BODY8("v_sad_u8 %0, %1, %2, %0"))
+MIXPROBE(m_salu16, SBODY8 SBODY8)
+MIXPROBE(m_v16_s16, BODY8("v_sad_u8 %0, %1, %2, %0") SBODY8 BODY8("v_sad_u8 %0, %1, %2, %0") SBODY8)
+MIXPROBE(m_v16_s8, BODY8("v_sad_u8 %0, %1, %2, %0") SBODY8 BODY8("v_sad_u8 %0, %1, %2, %0"))
+MIXPROBE(m_add16_s16, BODY8("v_add_u32 %0, %1, %0") SBODY8 BODY8("v_add_u32 %0, %1, %0") SBODY8)
+
 using K = void (*)(uint32_t*, uint64_t*);
 struct P { const char* name; K k; };
 
@@ -94,6 +141,24 @@ int main() {
             const double med = (double)c[c.size() / 2];
             // one wave's loop spans med cycles; wps waves share the SIMD
             printf(" %8.2f", med / insn_per_wave / wps);
+        }
+        printf("\n");
+    }
+    const P mixes[] = {{"16 sad", m_valu16}, {"16 s_add", m_salu16}, {"16 sad+16 s_add", m_v16_s16},
+                       {"16 sad+8 s_add", m_v16_s8}, {"16 v_add+16 s_add", m_add16_s16}, {"16 sad(sgpr src)", m_sad_sgpr},
+                       {"16 cndmask vcc", m_cnd_mask}, {"16 cndmask sgpr", m_cnd_e64}, {"16 mov_dpp", m_mov_dpp}};
+    printf("\nmixed streams: cycles per loop iteration per SIMD\n");
+    for (const P& p : mixes) {
+        printf("%-20s", p.name);
+        for (int wps : {1, 2, 3, 4}) {
+            const int blocks = cus * wps;
+            std::vector<uint64_t> c(blocks * 4);
+            hipLaunchKernelGGL(p.k, dim3(blocks), dim3(256), 0, 0, out, cyc);
+            hipLaunchKernelGGL(p.k, dim3(blocks), dim3(256), 0, 0, out, cyc);
+            hipDeviceSynchronize();
+            hipMemcpy(c.data(), cyc, c.size() * 8, hipMemcpyDeviceToHost);
+            std::nth_element(c.begin(), c.begin() + c.size() / 2, c.end());
+            printf(" %8.2f", (double)c[c.size() / 2] / ITER / wps);
         }
         printf("\n");
     }

@@ -27,7 +27,7 @@
 //     column) into a per-wave ring of NB row buffers, PD rows ahead, so input
 //     latency is hidden without registers; L rows come through the scalar
 //     cache one row ahead, border replication as compile-time byte maps.
-//   * the NW waves' partial minima are combined through LDS every kRB rows.
+//   * the NW waves' partial minima are combined through LDS every WIN rows.
 // Integer arithmetic only: bit-exact with the oracle by construction.
 #include <type_traits>
 #include <utility>
@@ -37,10 +37,6 @@
 namespace usv {
 namespace {
 
-#ifndef USV_KRB
-#define USV_KRB 8
-#endif
-constexpr int kRB = USV_KRB;  // output rows buffered between cross-wave combines
 constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_XCD_REMAP
 #define USV_XCD_REMAP 1  // XCD-contiguous tile order (0: plain linear order, for A/B runs)
@@ -54,7 +50,7 @@ constexpr int kK = 16;  // outputs per x-tile
 #define USV_EXP 0
 #endif
 #ifndef USV_SPLIT_CHAIN
-#define USV_SPLIT_CHAIN 1  // two independent prefix chains per row (ILP); 0: one chain
+#define USV_SPLIT_CHAIN 0  // 1: two independent prefix chains per row (ILP); 0: one chain
 #endif
 #ifndef USV_FAST_OCC
 #define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
@@ -72,15 +68,21 @@ struct Cfg {
     static constexpr int NR = NW * 63 + NPOS_V;  // R entries a wave reads per row
     static constexpr int NQ = (NR + 63) / 64;    // DMA instructions per R row
     static constexpr int NRS = NQ * 64;          // row-buffer stride (entries)
-    static constexpr int NB = NW >= 4 ? 4 : 8;   // row buffers per wave
+    // Row buffers per wave.  With one or two waves the ring holds WIN rows, so
+    // in the row loop (unrolled WIN times) every buffer index, LDS offset and
+    // M0 value is a compile-time constant; four waves keep a 4-row ring.
+    static constexpr bool STATIC_RING = NW <= 2;
+    static constexpr int NB = STATIC_RING ? WIN : 4;
     static constexpr int PD = NB - 1;            // rows in flight ahead of the one computed
+    static constexpr int KRB = WIN;              // output rows per cross-wave combine
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - RAD) mod 4, x0 % 4 == 0
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
     static constexpr int COMB_OFF = RBUF_OFF + NW * NB * NRS;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * kRB * NW * K;
+    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
     static_assert(RAD >= 1 && RAD <= 7, "packed-u16 cost needs w <= 15");
+    static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
 };
 
 // Where a tile's L row segment comes from.  Every tile reads its L bytes from
@@ -118,32 +120,45 @@ constexpr int kRowHalfMirror = 0x141;
 constexpr int kQuadSwap2 = 0x4E;  // quad_perm [2,3,0,1]
 constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]
 
-// 16 keys (64-lane vectors over disparities) -> every lane of 16-lane row q
-// holds the min keys of pixels 4q .. 4q+3 in out[0..3].
-// Two transposing swaps (lanes l, l^32 then l, l^16) halve the key count per
-// round; the last 4 keys are then min-all-reduced inside each row by four DPP
-// rounds (mirror, half-mirror, quad xor 2, quad xor 1: every lane meets all
-// 16), which needs no per-lane selects (v_cndmask is ~4x a VALU slot here).
-__device__ __forceinline__ void reduce16(const uint32_t (&k)[16], uint32_t (&out)[4]) {
+// v_cndmask with an explicit SGPR-pair lane mask (a VCC-sourced select issues
+// several times slower on gfx950: scripts/probes/valu_rate.hip).
+__device__ __forceinline__ uint32_t sel_mask(uint32_t if0, uint32_t if1, uint64_t mask) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(mask));
+    return r;
+}
+
+// 16 keys (cost << 8 | d, 64-lane vectors over disparities) -> lane l holds
+// the min key of pixel l >> 2 (ties -> smaller d):
+//  1. lanes l, l^32: permlane32 swap + min: lanes < 32 keep pixels 0-7;
+//  2. lanes l, l^16: permlane16 swap + min: 16-lane row q keeps 4q .. 4q+3;
+//  3. inside rows two transposing DPP rounds (mirror, half-mirror) and two
+//     quad rounds.
+template <int CTRL>
+__device__ __forceinline__ uint32_t tr_round(uint32_t a, uint32_t b, uint64_t hi_mask) {
+    // lanes in hi_mask keep b's pixel, the others a's; min with the DPP partner
+    return min(sel_mask(a, b, hi_mask), dpp<CTRL>(sel_mask(b, a, hi_mask)));
+}
+__device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16]) {
     uint32_t r1[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         auto p = __builtin_amdgcn_permlane32_swap(k[i], k[i + 8], false, false);
         r1[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // lanes 0-31: pixel i, 32-63: pixel i+8
     }
+    uint32_t r2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         auto p = __builtin_amdgcn_permlane16_swap(r1[i], r1[i + 4], false, false);
-        out[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 4q
+        r2[i] = min((uint32_t)p[0], (uint32_t)p[1]);  // 16-lane row q: pixel i + 4q
     }
+    constexpr uint64_t kBit3 = 0xFF00FF00FF00FF00ull, kBit2 = 0xF0F0F0F0F0F0F0F0ull;
+    uint32_t r3[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kRowMirror>(out[i]));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kRowHalfMirror>(out[i]));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kQuadSwap2>(out[i]));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = min(out[i], dpp<kQuadSwap1>(out[i]));
+    for (int i = 0; i < 2; ++i) r3[i] = tr_round<kRowMirror>(r2[i], r2[i + 2], kBit3);
+    uint32_t r4 = tr_round<kRowHalfMirror>(r3[0], r3[1], kBit2);
+    r4 = min(r4, dpp<kQuadSwap2>(r4));
+    return min(r4, dpp<kQuadSwap1>(r4));
 }
 
 // k-th vector read of a row in order of first use by the packed chain:
@@ -185,6 +200,12 @@ __device__ __forceinline__ void dma_u8(const uint8_t* row, uint32_t voff, uint32
     asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_ubyte %0, %1"
                  :: "v"(voff), "s"(row), "s"(m0) : "memory", "m0");
 }
+template <uint32_t OFF>
+__device__ __forceinline__ void dma_u8_at(const uint8_t* row, uint32_t voff, uint32_t lds_base) {
+    asm volatile("s_add_u32 m0, %2, %3\n\tglobal_load_lds_ubyte %0, %1"
+                 :: "v"(voff), "s"(row), "s"(lds_base), "n"(OFF) : "memory", "m0", "scc");
+}
+
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
 // vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
@@ -270,12 +291,15 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     using C = Cfg<RAD, NW>;
     using LS = LSeg<RAD, EDGE>;
     using LWords = typename SWords<LS::NLD>::T;
-    constexpr int WIN = C::WIN, K = C::K, HALF = C::HALF;
+    constexpr int WIN = C::WIN, K = C::K, HALF = C::HALF, NB = C::NB, PD = C::PD, KRB = C::KRB;
     constexpr int NDMA = C::NQ;  // VMEM ops issued per input row
-    const int l_eff = min(lane, (a.D - 1 - wave) / NW);
+    // lane l owns d = NW*l + wave; lanes past D-1 replay the wave's last valid
+    // disparity (same data, same key: they cannot change the argmin)
+    const int lmax = (a.D - 1 - wave) / NW;
+    const int l_eff = min(lane, lmax);
     const uint32_t d_eff = (uint32_t)(NW * l_eff + wave);
     const int cbase = x0 - RAD - (NW * 63 + wave);  // first R column this wave stages
-    uint32_t* rbuf = smem + C::RBUF_OFF + wave * C::NB * C::NRS;
+    uint32_t* rbuf = smem + C::RBUF_OFF + wave * NB * C::NRS;
     uint32_t* comb = smem + C::COMB_OFF;
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
@@ -296,12 +320,20 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
     for (int i = 0; i < C::NQ; ++i) colR[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1);
     const uint32_t rbase = lds_addr(rbuf);
-    auto issue_dma = [&](int t) {
-        const int buf = t & (C::NB - 1);
+    // BUF >= 0: compile-time ring slot (static ring); BUF < 0: slot t & (NB-1)
+    auto issue_dma = [&](int t, auto buf_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
         const uint8_t* rr = row_ptr(R, t);
+        if constexpr (BUF >= 0) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                ((USV_EXP != 1 ? dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase) : void()), ...);
+            }(std::make_integer_sequence<int, C::NQ>{});
+        } else {
+            const int buf = t & (NB - 1);
 #pragma unroll
-        for (int i = 0; i < C::NQ; ++i)
-            if (USV_EXP != 1) dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
+            for (int i = 0; i < C::NQ; ++i)
+                if (USV_EXP != 1) dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
+        }
     };
 
     // ---- L bytes: the row segment through the scalar cache, one row ahead.
@@ -311,19 +343,26 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     LWords lw_next;
     auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(row_ptr(L, t) + LS::base(x0)); };
 
-    // One input row t: packed chain, H pairs, S / ring update.
 #if USV_STAMPS
     Stamps st;
     st.t_begin = st.last = Stamps::now();
 #endif
-    auto do_row = [&](int t, auto warm_tag, auto slot_tag, uint32_t(&S)[HALF],
-                      uint32_t(&ring)[WIN][HALF]) {
+    // One input row t = t0 + I (t0 a multiple of WIN): packed chain, H pairs,
+    // S / ring update.  I selects the ring slot (and, with the static ring,
+    // the row buffers) at compile time.
+    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[HALF], uint32_t(&ring)[WIN][HALF]) {
         constexpr bool WARM = decltype(warm_tag)::value;
-        constexpr int SL = decltype(slot_tag)::value;
-        const int buf = t & (C::NB - 1);
-        wait_vmcnt<(C::PD - 1) * NDMA>();  // row t has landed in LDS
+        constexpr int I = decltype(i_tag)::value;
+        // opaque row index: keeps the compiler from computing every unrolled
+        // row's pointers up front (SGPR pressure that ends in VGPR spills)
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        wait_vmcnt<(PD - 1) * NDMA>();  // row t has landed in LDS
         __builtin_amdgcn_wave_barrier();
-        issue_dma(t + C::PD);
+        if constexpr (C::STATIC_RING)
+            issue_dma(t + PD, std::integral_constant<int, (I + PD) % NB>{});
+        else
+            issue_dma(t + PD, std::integral_constant<int, -1>{});
         USV_STAMP(0);
 
         uint32_t Lv[C::NPOS];
@@ -341,7 +380,12 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         }
 
         using VT = typename VecT<C::VEC>::T;
-        const VT* rb = reinterpret_cast<const VT*>(rbuf + buf * C::NRS + s_l);
+        // Row-buffer offset as an opaque scalar: one v_add per row, instead
+        // of the compiler keeping a VGPR base per static ring slot (the
+        // ds_read2 offset field only spans 2 KB) live through the loop.
+        int boff = (C::STATIC_RING ? I % NB : (t & (NB - 1))) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
         uint32_t Rv[C::NPOS_V];
         // issue the reads in the chain's order of use (step j needs columns j
         // and j + HALF) so the first steps only wait for the first reads
@@ -353,10 +397,10 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
             for (int e = 0; e < C::VEC; ++e) Rv[jv * C::VEC + e] = vget<C::VEC>(v, e);
         }
-        // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)], split
-        // into two independent chains for ILP: A covers steps [0, SP), B
+        // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)]; with
+        // USV_SPLIT_CHAIN two independent chains: A covers steps [0, SP), B
         // steps [SP, NSTEP) from zero, so P[j] = A[SP] + B[j - SP] for j > SP.
-        constexpr int SP = USV_SPLIT_CHAIN ? HALF : C::NSTEP;  // 0: one serial chain (B empty)
+        constexpr int SP = USV_SPLIT_CHAIN ? HALF : C::NSTEP;
         constexpr int NB_STEPS = C::NSTEP - SP;
         uint32_t A[SP + 1], Bc[NB_STEPS + 1];
         A[0] = 0;
@@ -374,18 +418,17 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         }
 #pragma unroll
         for (int x = 0; x < HALF; ++x) {
-            // H pair (x, x + HALF) = P[x + WIN] - P[x]
+            // H pair (x, x + HALF) = P[x + WIN] - P[x].  Packed pairs, but
+            // every intermediate half stays in [0, 65535] (prefixes are
+            // monotone, S - ring is a w-1 row sum), so plain 32-bit add/sub
+            // give the packed result exactly: v_add/v_sub_u32 issue at full
+            // rate, v_pk_*_u16 at half rate (scripts/probes/valu_rate.hip).
             uint32_t h;
-            // Packed pairs, but every intermediate half stays in [0, 65535]
-            // (prefixes are monotone, S - ring is a w-1 row sum), so plain
-            // 32-bit add/sub give the packed result exactly: v_add/v_sub_u32
-            // issue at full rate, v_pk_*_u16 at half rate on gfx950
-            // (scripts/probes/valu_rate.hip).
             if (x + WIN <= SP) h = A[x + WIN] - A[x];
             else h = Bc[x + WIN - SP] + (A[SP] - A[x]);
             if constexpr (WARM) S[x] = S[x] + h;
-            else S[x] = (S[x] - ring[SL][x]) + h;
-            ring[SL][x] = h;
+            else S[x] = (S[x] - ring[I][x]) + h;
+            ring[I][x] = h;
         }
         // The row's LDS reads are all consumed: request row t+1's L words now,
         // so the lgkmcnt waits of this row's LDS reads never retire (and wait
@@ -396,57 +439,56 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         st.rows++;
 #endif
         load_lw(t + 1);
-        // Keep rows apart: interleaving the unrolled warm-up rows only raises
+        // Keep rows apart: interleaving the unrolled rows only raises
         // register pressure (spills whose reloads would drain the DMA queue).
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // ---- output: per-row keys -> LDS, cross-wave min every kRB rows ----
-    int slot = 0, cb = 0, y_chunk = y_begin;
-    auto flush = [&]() {
+    // ---- output: per-row keys -> LDS, cross-wave min every KRB rows ----
+    // Output row o goes to combine slot o % KRB; with KRB = WIN the flush
+    // points sit at fixed positions of the WIN-unrolled row loop.
+    int cb = 0, y_chunk = y_begin;
+    auto flush = [&](int rows) {
         if (USV_EXP != 2) lds_barrier();
-        const int items = slot * K;
-        for (int i = threadIdx.x; i < items; i += NW * 64) {
+        // opaque thread id: the flush's per-lane addresses must not be hoisted
+        // out of the row loop (they would stay live through it and spill)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int items = rows * K;
+        for (int i = tid; i < items; i += NW * 64) {
             const int row = i / K, p = i - row * K;
             uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * kRB + row) * NW + w2) * K + p]);
-            const int x = x0 + p;
-            if (x < a.W) {
-                const uint32_t dv = key & 0xFFu;
-                const size_t y = (size_t)(y_chunk + row);
-                disp[y * a.disp_pitch + x] = (uint8_t)dv;
-                if (dist) dist[y * a.dist_pitch + x] = lut_s[dv];
-            }
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
+            const uint32_t dv = key & 0xFFu;
+            const size_t y = (size_t)(y_chunk + row);
+            disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
+            if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
         }
-        y_chunk += slot;
-        slot = 0;
+        y_chunk += rows;
         cb ^= 1;
     };
-    auto emit = [&](const uint32_t(&S)[HALF], bool last) {
+    auto emit = [&](const uint32_t(&S)[HALF], int slot) {
         uint32_t keys[K];
 #pragma unroll
         for (int i = 0; i < HALF; ++i) {
             keys[i] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c050400u);         // (S.lo << 8) | d
             keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
         }
-        uint32_t m[4];
+        uint32_t m;
         if constexpr (USV_EXP == 3) {
-            m[0] = m[1] = m[2] = m[3] = keys[0];
+            m = keys[0];
 #pragma unroll
-            for (int i = 1; i < K; ++i) m[i & 3] ^= keys[i];
+            for (int i = 1; i < K; ++i) m ^= keys[i];
         } else {
-            reduce16(keys, m);
+            m = reduce16(keys);
         }
-        if ((lane & 15) == 0)  // one lane per 16-lane row stores its 4 pixels
-            *reinterpret_cast<uint4*>(comb + ((cb * kRB + slot) * NW + wave) * K + (lane >> 2)) =
-                make_uint4(m[0], m[1], m[2], m[3]);
-        ++slot;
+        // the 4 lanes of a quad hold the same key: same value, same address
+        comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 2)] = m;
         USV_STAMP(3);
-        if (slot == kRB || last) {
-            flush();
-            USV_STAMP(4);
-        }
+        // the next row's loads must not be hoisted into the reduction (the
+        // rows are one basic block now: keys + R values + ring would spill)
+        __builtin_amdgcn_sched_barrier(0);
     };
 
     uint32_t S[HALF];
@@ -454,29 +496,41 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     for (int i = 0; i < HALF; ++i) S[i] = 0;
     uint32_t ring[WIN][HALF];
 
-    // prologue: PD rows in flight, L words of rows 0 and 1 requested
-#pragma unroll
-    for (int t = 0; t < C::PD; ++t) issue_dma(t);
+    // prologue: PD rows in flight, L words of row 0 requested
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+        (issue_dma(P, std::integral_constant<int, C::STATIC_RING ? P : -1>{}), ...);
+    }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
 
     using WarmT = std::integral_constant<bool, true>;
     using SteadyT = std::integral_constant<bool, false>;
-    // ---- warm-up: the first WIN input rows fill the ring ----
+    // ---- warm-up: the first WIN input rows fill the ring; output row 0 ----
     [&]<int... I>(std::integer_sequence<int, I...>) {
         (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
     }(std::make_integer_sequence<int, WIN>{});
-    emit(S, nout == 1);
+    emit(S, 0);
 
-    // ---- steady state: one output row per input row ----
+    // ---- steady state: input row t0 + I -> output row t0 + I - 2r, slot (I + 1) % WIN
+    auto step = [&](int t0, auto i_tag) {
+        constexpr int I = decltype(i_tag)::value;
+        do_row(t0 + I, SteadyT{}, i_tag, S, ring);
+        emit(S, (I + 1) % WIN);
+        if constexpr ((I + 1) % WIN == KRB - 1) {
+            flush(KRB);
+            USV_STAMP(4);
+        }
+    };
+    // (the per-row guard also splits the group into basic blocks: one
+    // 2000-instruction block makes the register allocator spill the ring)
     for (int t0 = WIN; t0 < T; t0 += WIN) {
-        bool done = false;
         [&]<int... I>(std::integer_sequence<int, I...>) {
-            ((done = done || (t0 + I >= T),
-              done ? void() : (do_row(t0 + I, SteadyT{}, std::integral_constant<int, I>{}, S, ring),
-                               emit(S, t0 + I == T - 1))),
-             ...);
+            bool go = true;
+            ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
         }(std::make_integer_sequence<int, WIN>{});
     }
+    // rows emitted since the last flush: outputs o with o % WIN in [0, rest)
+    const int rest = nout % KRB;
+    if (rest) flush(rest);
     wait_vmcnt<0>();  // drain the look-ahead DMAs before the wave retires
 #if USV_STAMPS
     if (lane == 0) {
