@@ -79,3 +79,11 @@ def test_split_scalar_loads_do_not_clobber_their_base(fast_kernels):
             m2 = re.match(r"s_load_dword(?:x2)? (\S+), (\S+), 0x10$", b)
             if m1 and m2 and m1.group(2) == m2.group(2):
                 assert not (_sregs(m1.group(1)) & _sregs(m2.group(2))), (name, a, b)
+
+
+def test_lds_dma_m0_wait_state(fast_kernels):
+    # GFX9: an SALU write of M0 needs one wait state before an LDS-DMA reads it
+    for name, ins in fast_kernels.items():
+        for a, b in zip(ins, ins[1:]):
+            if b.startswith("global_load_lds"):
+                assert not re.match(r"s_\w+ m0,", a), (name, a, b)

@@ -190,19 +190,21 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // LDS-DMA of one byte per lane (zero-extended to a dword at M0 + 4*lane),
-// saddr form: scalar row base + 32-bit lane offset.  Inline asm so the
+// saddr form: scalar row base + 32-bit lane offset.  GFX9 needs one wait
+// state between an SALU write of M0 and an LDS-DMA that reads it (the
+// compiler's hazard recognizer does not look inside inline asm): s_nop 0.  Inline asm so the
 // compiler cannot precompute 64-bit per-lane addresses for the look-ahead
 // rows (it hoisted and spilled them); the vmcnt waits are all explicit.
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
 }
 __device__ __forceinline__ void dma_u8(const uint8_t* row, uint32_t voff, uint32_t m0) {
-    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_ubyte %0, %1"
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
                  :: "v"(voff), "s"(row), "s"(m0) : "memory", "m0");
 }
 template <uint32_t OFF>
 __device__ __forceinline__ void dma_u8_at(const uint8_t* row, uint32_t voff, uint32_t lds_base) {
-    asm volatile("s_add_u32 m0, %2, %3\n\tglobal_load_lds_ubyte %0, %1"
+    asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
                  :: "v"(voff), "s"(row), "s"(lds_base), "n"(OFF) : "memory", "m0", "scc");
 }
 
