@@ -16,6 +16,6 @@ step() {  # step <name> <timeout> <cmd...>
   return 0
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step bench 300 python bench.py --steps 50 --warmup 10
 exit 0

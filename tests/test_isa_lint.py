@@ -40,8 +40,19 @@ def _disassembly(tmp_path):
             cur = m.group(1)
             funcs[cur] = []
         elif cur and line.startswith("\t"):
-            funcs[cur].append(line.split("//")[0].strip())
+            code, _, comment = line.partition("//")
+            a = re.match(r"\s*([0-9A-F]+):", comment)
+            funcs[cur].append(Insn(code.strip(), int(a.group(1), 16) if a else -1))
     return funcs
+
+
+class Insn(str):
+    """An instruction's text (a str, so the simple checks compare text) plus its byte address."""
+
+    def __new__(cls, text, addr):
+        o = super().__new__(cls, text)
+        o.addr = addr
+        return o
 
 
 def _sregs(tok):
@@ -79,6 +90,64 @@ def test_split_scalar_loads_do_not_clobber_their_base(fast_kernels):
             m2 = re.match(r"s_load_dword(?:x2)? (\S+), (\S+), 0x10$", b)
             if m1 and m2 and m1.group(2) == m2.group(2):
                 assert not (_sregs(m1.group(1)) & _sregs(m2.group(2))), (name, a, b)
+
+
+def _successors(ins):
+    at = {i.addr: k for k, i in enumerate(ins)}
+    out = []
+    for k, i in enumerate(ins):
+        m = re.match(r"s_(c?)branch\w* (\d+)", i)
+        if m:
+            off = int(m.group(2))
+            off = off - 65536 if off >= 32768 else off
+            s = [at[i.addr + 4 + 4 * off]] if i.addr + 4 + 4 * off in at else []
+            if m.group(1):
+                s.append(k + 1)
+        elif i.startswith(("s_endpgm", "s_setpc_b64")):
+            s = []
+        else:
+            s = [k + 1]
+        out.append([j for j in s if j < len(ins)])
+    return out
+
+
+def inflight_scalar_load_hazards(ins):
+    """Instructions that touch an SGPR while a scalar load writing it may still be in flight.
+
+    A scalar load writes its destination whenever its data returns; only
+    s_waitcnt lgkmcnt(0) retires it (they return out of order).  The hand-written
+    s_load of the next row's L words is invisible to the compiler's waitcnt
+    pass, so on a path where that value is dead (the loop exit) the compiler may
+    reuse the registers -- the late return then clobbered the flush's row count.
+    Forward dataflow over the CFG: the set of in-flight SGPRs at each instruction.
+    """
+    succ = _successors(ins)
+    state = [None] * len(ins)
+    state[0] = frozenset()
+    work, bad = [0], set()
+    while work:
+        k = work.pop()
+        cur, i = set(state[k]), ins[k]
+        toks = i.replace(",", " ").split()
+        if i.startswith("s_waitcnt") and "lgkmcnt(0)" in i:
+            cur = set()
+        elif i.startswith("s_load"):
+            if _sregs(toks[2]) & cur:
+                bad.add((k, str(i)))
+            cur |= _sregs(toks[1])
+        elif any(_sregs(t) & cur for t in toks[1:]):
+            bad.add((k, str(i)))
+        fs = frozenset(cur)
+        for j in succ[k]:
+            if state[j] is None or not fs <= state[j]:
+                state[j] = fs if state[j] is None else state[j] | fs
+                work.append(j)
+    return sorted(bad)
+
+
+def test_no_sgpr_use_while_scalar_load_in_flight(fast_kernels):
+    bad = {k: inflight_scalar_load_hazards(v)[:3] for k, v in fast_kernels.items()}
+    assert not any(bad.values()), {k: v for k, v in bad.items() if v}
 
 
 def test_lds_dma_m0_wait_state(fast_kernels):

@@ -530,6 +530,11 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
         }(std::make_integer_sequence<int, WIN>{});
     }
+    // The last row requested row T's L words, which nothing reads.  Retire that
+    // scalar load before its destination SGPRs can be reused: it writes them
+    // whenever its data returns (a late return clobbered the flush's row count
+    // and pointers -- an illegal address on the GPU; tests/test_isa_lint.py).
+    wait_lgkm0<LS::NLD>(lw_next);
     // rows emitted since the last flush: outputs o with o % WIN in [0, rest)
     const int rest = nout % KRB;
     if (rest) flush(rest);
