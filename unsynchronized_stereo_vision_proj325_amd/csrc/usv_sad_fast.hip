@@ -45,12 +45,19 @@ constexpr int kK = 16;  // outputs per x-tile
 #define USV_STAMPS 0  // diagnostic build: per-phase s_memtime totals (scripts/stamps.py)
 #endif
 // Timing experiments only (wrong results): USV_EXP=1 no R DMA, 2 no flush
-// barrier, 3 trivial reduction.  Never set in the product build.
+// barrier, 3 trivial reduction, 4 no L byte extraction,
+// 5 xor/add chain instead of v_sad, 7 no reduction.  Never set in the product build.
 #ifndef USV_EXP
 #define USV_EXP 0
 #endif
 #ifndef USV_SPLIT_CHAIN
 #define USV_SPLIT_CHAIN 0  // 1: two independent prefix chains per row (ILP); 0: one chain
+#endif
+#ifndef USV_STATIC_RING
+#define USV_STATIC_RING 0  // 1: WIN-slot R ring with compile-time slots (more LDS); 0: 8-slot dynamic ring
+#endif
+#ifndef USV_RED_LDS
+#define USV_RED_LDS 1  // argmin transpose through LDS (1) or permlane/DPP rounds (0)
 #endif
 #ifndef USV_FAST_OCC
 #define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
@@ -71,14 +78,19 @@ struct Cfg {
     // Row buffers per wave.  With one or two waves the ring holds WIN rows, so
     // in the row loop (unrolled WIN times) every buffer index, LDS offset and
     // M0 value is a compile-time constant; four waves keep a 4-row ring.
-    static constexpr bool STATIC_RING = NW <= 2;
-    static constexpr int NB = STATIC_RING ? WIN : 4;
+    static constexpr bool STATIC_RING = USV_STATIC_RING && NW <= 2;
+    static constexpr int NB = STATIC_RING ? WIN : (NW <= 2 ? 8 : 4);
     static constexpr int PD = NB - 1;            // rows in flight ahead of the one computed
     static constexpr int KRB = WIN;              // output rows per cross-wave combine
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - RAD) mod 4, x0 % 4 == 0
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
-    static constexpr int COMB_OFF = RBUF_OFF + NW * NB * NRS;
+    // per-wave argmin transpose buffer: 16 pixels x 64 keys (USV_RED_LDS)
+    static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
+    // (r = 6 with two waves sits at the 168-VGPR limit: the DPP rounds need fewer registers)
+    static constexpr bool RED_LDS = USV_RED_LDS && !(RAD == 6 && NW == 2);
+    static constexpr int TB_WORDS = RED_LDS ? K * 64 : 0;
+    static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
     static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
     static_assert(RAD >= 1 && RAD <= 7, "packed-u16 cost needs w <= 15");
@@ -159,6 +171,35 @@ __device__ __forceinline__ uint32_t reduce16(const uint32_t (&k)[16]) {
     uint32_t r4 = tr_round<kRowHalfMirror>(r3[0], r3[1], kBit2);
     r4 = min(r4, dpp<kQuadSwap2>(r4));
     return min(r4, dpp<kQuadSwap1>(r4));
+}
+
+// The same reduction through LDS (no permlane / DPP rounds but the last two):
+// lane l stores key p at tb[64 p + l] (pixel-major: eight ds_write2st64), then
+// lane m = 4p + q reads the 16 keys of pixel p from lanes 16q .. 16q+15 as
+// four 16-byte windows, visiting them in the rotated order (k + p) & 3 so that
+// the 16 lanes of each read phase touch 16 distinct bank quads; a v_min3 tree
+// and two quad DPP rounds finish.  The wave's own LDS ops run in order, so the
+// next row's stores cannot overtake this row's reads.
+__device__ __forceinline__ uint32_t reduce16_lds(const uint32_t (&k)[16], uint32_t* tb, int lane,
+                                                 const uint32_t (&rd)[4]) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) tb[64 * p + lane] = k[p];
+    asm volatile("" ::: "memory");
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 q = reinterpret_cast<const uint4*>(tb)[rd[j]];
+        v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+    }
+    asm volatile("" ::: "memory");
+    uint32_t a = min(min(v[0], v[1]), v[2]), b = min(min(v[3], v[4]), v[5]);
+    uint32_t c = min(min(v[6], v[7]), v[8]), d = min(min(v[9], v[10]), v[11]);
+    uint32_t e = min(min(v[12], v[13]), v[14]);
+    a = min(min(a, b), c);
+    d = min(min(d, e), v[15]);
+    uint32_t r = min(a, d);
+    r = min(r, dpp<kQuadSwap2>(r));
+    return min(r, dpp<kQuadSwap1>(r));
 }
 
 // k-th vector read of a row in order of first use by the packed chain:
@@ -303,6 +344,14 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     const int cbase = x0 - RAD - (NW * 63 + wave);  // first R column this wave stages
     uint32_t* rbuf = smem + C::RBUF_OFF + wave * NB * C::NRS;
     uint32_t* comb = smem + C::COMB_OFF;
+    uint32_t* tb = smem + C::TB_OFF + wave * C::TB_WORDS;
+    // transposed-read windows (uint4 index): lane m = 4p + q, window j visited as (j + p) & 3
+    uint32_t rd[4];
+    {
+        const int p = lane >> 2, q = lane & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rd[j] = (uint32_t)(16 * p + 4 * q + ((j + p) & 3));
+    }
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
     const int nout = y_end - y_begin;
@@ -377,7 +426,8 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
             for (int j = 0; j < C::NPOS; ++j) {
                 const int bidx = LS::byte(j);
-                Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+                if constexpr (USV_EXP == 4) Lv[j] = lw[(bidx >> 2) & 7];  // timing only: no byte extraction
+                else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
 
@@ -409,9 +459,13 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         Bc[0] = 0;
 #pragma unroll
         for (int j = 0; j < (SP > NB_STEPS ? SP : NB_STEPS); ++j) {
-            if (j < SP)
-                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
-                                                      __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
+            if (j < SP) {
+                if constexpr (USV_EXP == 5)  // timing only: same dependency depth, plain adds
+                    A[j + 1] = (A[j] + (Lv[j + HALF] ^ Rv[j + HALF])) + (Lv[j] ^ Rv[j]);
+                else
+                    A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
+                                                          __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
+            }
             if (j < NB_STEPS) {
                 const int jj = j + SP;
                 Bc[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[jj + HALF], Rv[jj + HALF],
@@ -478,10 +532,14 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
         }
         uint32_t m;
-        if constexpr (USV_EXP == 3) {
+        if constexpr (USV_EXP == 7) {
+            m = keys[lane & 15];  // timing only: no cross-lane reduction at all
+        } else if constexpr (USV_EXP == 3) {
             m = keys[0];
 #pragma unroll
             for (int i = 1; i < K; ++i) m ^= keys[i];
+        } else if constexpr (C::RED_LDS) {
+            m = reduce16_lds(keys, tb, lane, rd);
         } else {
             m = reduce16(keys);
         }
