@@ -147,6 +147,23 @@ def test_batch_launch(gpu):
     assert np.array_equal(dist.cpu().numpy(), lut[disp])
 
 
+@pytest.mark.parametrize("B,W,H,D,w", [(2, 1920, 1080, 128, 11),  # 240 columns: XCD-contiguous runs
+                                       (1, 1000, 700, 100, 9),    # 63 columns: linear column order
+                                       (3, 640, 480, 64, 7)])     # one-wave workgroups, 120 columns
+def test_weighted_band_plan(gpu, B, W, H, D, w):
+    """Full-occupancy launches take generation-weighted band heights
+    (csrc/usv_sad_fast.hip BandPlan): every row of every pair still written once, bit-exact."""
+    pairs = [synthetic_pair(W, H, D, pair_index=20 + i, noise=2) for i in range(B)]
+    L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    R = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    out = torch.full((B, H, W), 255, dtype=torch.uint8, device=gpu)
+    StereoBlockMatcher(D, w).compute(L, R, out_disp=out)
+    got = out.cpu().numpy()
+    for i, (l, r, _) in enumerate(pairs):
+        ref = oracle_sad(l, r, D, w, "sad", "sliding", threads=THREADS)
+        assert np.array_equal(got[i], ref), (i, _mismatch(got[i], ref))
+
+
 def test_fused_distance_bitexact(gpu):
     L, R, _ = synthetic_pair(1920, 1080, 128, pair_index=3)
     disp, dist = gpu_disp(gpu, L, R, 128, 11, with_distance=True)

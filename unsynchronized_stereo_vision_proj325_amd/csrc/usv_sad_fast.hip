@@ -38,9 +38,6 @@ namespace usv {
 namespace {
 
 constexpr int kK = 16;  // outputs per x-tile
-#ifndef USV_XCD_REMAP
-#define USV_XCD_REMAP 1  // XCD-contiguous tile order (0: plain linear order, for A/B runs)
-#endif
 #ifndef USV_STAMPS
 #define USV_STAMPS 0  // diagnostic build: per-phase s_memtime totals (scripts/stamps.py)
 #endif
@@ -49,6 +46,19 @@ constexpr int kK = 16;  // outputs per x-tile
 // 5 xor/add chain instead of v_sad, 7 no reduction.  Never set in the product build.
 #ifndef USV_EXP
 #define USV_EXP 0
+#endif
+#ifndef USV_PRIO
+// Wave-priority rotation.  The SIMD arbitrates VALU issue by priority, then
+// age: with equal priorities the oldest of the three resident waves runs
+// nearly unimpeded and the youngest finishes ~27 us later on config C
+// (scripts/wgtime.py), so the launch ends in a one- and two-wave tail.
+// 1: rotate s_setprio by the wave's slot on its SIMD every flush; 2: by the
+// workgroup index (both waves of a workgroup share a phase); 3: by slot,
+// every input row; 0: off.
+#define USV_PRIO 0
+#endif
+#ifndef USV_WGTIME
+#define USV_WGTIME 0  // diagnostic build: per-workgroup start/end s_memrealtime + hardware id (scripts/wgtime.py)
 #endif
 #ifndef USV_SPLIT_CHAIN
 #define USV_SPLIT_CHAIN 0  // 1: two independent prefix chains per row (ILP); 0: one chain
@@ -253,6 +263,18 @@ __device__ __forceinline__ void dma_u8_at(const uint8_t* row, uint32_t voff, uin
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
 // vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
 // stores, so lgkmcnt(0) before the barrier is all the hand-off needs.
+__device__ __forceinline__ void set_prio(int p) {
+    if (p == 0) __builtin_amdgcn_s_setprio(0);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(2);
+}
+// The wave's slot on its SIMD (HW_ID.WAVE_ID), wave-uniform.
+__device__ __forceinline__ int wave_slot() {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    return (int)(hw & 0xFu);
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -325,6 +347,11 @@ struct Stamps {
 #define USV_STAMP_SKIP() ((void)0)
 #endif
 
+#if USV_WGTIME
+// per workgroup: {start, end} (100 MHz realtime), HW_ID, XCC_ID, x-tile, band
+__device__ unsigned long long g_usv_wgtime[4096 * 8];
+#endif
+
 template <int RAD, int NW, int EDGE>
 __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
                                           const uint8_t* __restrict__ R,
@@ -354,6 +381,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     }
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
+    const int prio_slot = USV_PRIO == 3 ? wave_slot() : 0;
     const int nout = y_end - y_begin;
     const int T = nout + 2 * RAD;  // input rows walked
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
@@ -410,6 +438,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * NDMA>();  // row t has landed in LDS
         __builtin_amdgcn_wave_barrier();
+        if constexpr (USV_PRIO == 3) set_prio((prio_slot + t) % 3);
         if constexpr (C::STATIC_RING)
             issue_dma(t + PD, std::integral_constant<int, (I + PD) % NB>{});
         else
@@ -504,7 +533,10 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // Output row o goes to combine slot o % KRB; with KRB = WIN the flush
     // points sit at fixed positions of the WIN-unrolled row loop.
     int cb = 0, y_chunk = y_begin;
+    int prio_phase = USV_PRIO == 2 ? (int)blockIdx.x : (USV_PRIO == 1 || USV_PRIO == 3 ? wave_slot() : 0);
+    if (USV_PRIO) set_prio(prio_phase % 3);
     auto flush = [&](int rows) {
+        if (USV_PRIO == 1 || USV_PRIO == 2) set_prio(++prio_phase % 3);
         if (USV_EXP != 2) lds_barrier();
         // opaque thread id: the flush's per-lane addresses must not be hoisted
         // out of the row loop (they would stay live through it and spill)
@@ -607,6 +639,15 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #endif
 }
 
+// Band decomposition of one launch (launch_rn): m bands per column, their
+// heights weighted by dispatch generation (see sad_fast_kernel).
+struct BandPlan {
+    int n_xt;      // x-tiles per pair
+    int m;         // bands per column (pair, x-tile)
+    int gen_g;     // workgroups per dispatch generation per XCD (4 SIMDs x CUs per XCD / waves per WG)
+    unsigned weights;  // byte g: relative band height of generation g (g >= 3 use byte 3)
+};
+
 // r = 7 (15-row ring) and r = 6 with four waves need more than 168 VGPRs:
 // two waves per SIMD instead of spilling (tests/test_isa_lint.py checks).
 constexpr int fast_occ(int rad, int nw) { return (rad >= 7 || (rad == 6 && nw == 4)) ? 2 : USV_FAST_OCC; }
@@ -616,34 +657,56 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
                                                               const uint8_t* __restrict__ R,
                                                               uint8_t* __restrict__ disp,
                                                               double* __restrict__ dist,
-                                                              MatchArgs a, int band_rows, int n_xt,
-                                                              int n_bands) {
+                                                              MatchArgs a, BandPlan P) {
     using C = Cfg<RAD, NW>;
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // XCD-aware tile order.  Workgroups are dispatched round-robin over the 8
-    // XCDs (linear id mod 8), each with its own L2: renumber so XCD k owns the
-    // k-th contiguous run of (x-tile, band, pair) in x-fastest order.  Tiles of
-    // one band then share an L2 and every R/L row is fetched from HBM about
-    // once instead of once per XCD.  A bijection whatever the real placement.
+#if USV_WGTIME
+    const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    // Work map.  Workgroups are dispatched round-robin over the 8 XCDs
+    // (linear id mod 8), each with its own L2: XCD k owns the k-th contiguous
+    // run of tiles (x-tile fastest, then band, then pair), so the tiles of one
+    // band share an L2 and every L/R row is fetched about once.
+    // Band heights are weighted by dispatch generation: the SIMD arbitrates
+    // VALU issue by age, so with three resident waves per SIMD the first-
+    // dispatched generation of workgroups runs ~1.4x faster than the last
+    // (scripts/wgtime.py); equal bands end in a one- and two-wave tail.
+    // Generation of a tile = (its index in its XCD's run) / P.gen_g, weight =
+    // byte g of P.weights; a column's bands get heights proportional to the
+    // weights of the tiles that carry them.  Any placement keeps the map a
+    // bijection; only speed depends on the dispatch model.
     const unsigned total = gridDim.x, lin = blockIdx.x;
     const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-#if USV_XCD_REMAP
     const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
-#else
-    const unsigned tile = lin + 0u * (xcd + base + rem);
-#endif
-    const int xt = (int)(tile % (unsigned)n_xt);
-    const int band = (int)((tile / (unsigned)n_xt) % (unsigned)n_bands);
-    const size_t b = tile / ((unsigned)n_xt * (unsigned)n_bands);
+    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
+    const unsigned col_xt = tile % nxt, s = (tile / nxt) % (unsigned)P.m, pair = tile / per_pair;
+    const unsigned long_run = base + 1u, split = rem * long_run;
+    auto gen_weight = [&](unsigned sb) -> unsigned {
+        const unsigned t = pair * per_pair + sb * nxt + col_xt;  // tile carrying band sb of this column
+        const unsigned j = t < split ? t % long_run : (t - split) % base;
+        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
+        return (P.weights >> (8 * g)) & 0xFFu;
+    };
+    unsigned pre = 0, tot = 0;
+    for (unsigned sb = 0; sb < (unsigned)P.m; ++sb) {
+        const unsigned wgt = gen_weight(sb);
+        pre += sb < s ? wgt : 0u;
+        tot += wgt;
+    }
+    const unsigned col = pair * nxt + col_xt;
+    const int xt = (int)(col % (unsigned)P.n_xt);
+    const int band = (int)s;
+    const size_t b = col / (unsigned)P.n_xt;
     // x-tile origin: the last tile is aligned to the right border and the one
     // before it pulled left if needed, so only tiles 0 and n-1 clamp L.
     int x0 = xt * C::K;
+    const int n_xt = P.n_xt;
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
-    const int y_begin = band * band_rows;
-    const int y_end = min(a.H, y_begin + band_rows);
+    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
     L += b * a.pair_stride;
     R += b * a.pair_stride;
     disp += b * a.disp_stride;
@@ -653,12 +716,26 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
         for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
     }
     __syncthreads();
+    if (y_end <= y_begin) return;  // (uniform) an empty band: nothing to emit
     if (xt == 0)
         band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
     else if (xt == n_xt - 1)
         band_loop<RAD, NW, kRight>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
     else
         band_loop<RAD, NW, kInterior>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+#if USV_WGTIME
+    __syncthreads();
+    if (lane == 0 && blockIdx.x < 4096) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long* o = g_usv_wgtime + 8 * blockIdx.x + 4 * (wave & 1);
+        o[0] = wg_t0;
+        o[1] = __builtin_amdgcn_s_memrealtime();
+        o[2] = hw | ((unsigned long long)xcc << 32);
+        o[3] = (unsigned long long)xt | ((unsigned long long)band << 32);
+    }
+#endif
 }
 
 // Blocks resident per CU for this instantiation (queried once).
@@ -685,23 +762,36 @@ int cu_count() {
     return n;
 }
 
+// Relative band heights by dispatch generation, three resident waves per SIMD
+// (config C, profiles/probes/wgtime_*.txt: equal bands took 61.5 / 70.0 /
+// 84.0 us by generation; one refinement step of heights ~ 1/time).
+#ifndef USV_GEN_WEIGHTS
+#define USV_GEN_WEIGHTS 0x3F3F5564u  // 100, 85, 63, 63
+#endif
+
 template <int RAD, int NW>
 hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     constexpr int K = kK, WIN = 2 * RAD + 1;
-    const int n_xt = (a.W + K - 1) / K;
+    BandPlan P{};
+    P.n_xt = (a.W + K - 1) / K;
     // One round of resident workgroups: bands = slots / (x-tiles * pairs),
     // keeping bands at least 2w rows so the ring warm-up stays amortised.
-    const long slots = (long)cu_count() * resident_blocks_per_cu<RAD, NW>();
-    long n_bands = slots / ((long)n_xt * a.batch);
-    if (n_bands < 1) n_bands = 1;
-    int band_rows = (int)((a.H + n_bands - 1) / n_bands);
-    if (band_rows < 2 * WIN) band_rows = 2 * WIN;
-    n_bands = (a.H + band_rows - 1) / band_rows;
-    const long total = (long)n_xt * n_bands * a.batch;
+    const int per_cu = resident_blocks_per_cu<RAD, NW>();
+    const long slots = (long)cu_count() * per_cu;
+    const long NC = (long)P.n_xt * a.batch;
+    long m = slots / NC;
+    if (m < 1) m = 1;
+    if (m > a.H / (2 * WIN)) m = a.H / (2 * WIN) > 0 ? a.H / (2 * WIN) : 1;
+    P.m = (int)m;
+    const long total = NC * m;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
+    if (P.gen_g < 1) P.gen_g = 1;
+    // weighted only when every SIMD holds three waves of one round
+    const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
+    P.weights = three ? USV_GEN_WEIGHTS : 0x01010101u;
     dim3 grid((unsigned)total), block(NW * 64);
-    hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a,
-                       band_rows, n_xt, (int)n_bands);
+    hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
 }
 
@@ -722,6 +812,12 @@ extern "C" __attribute__((visibility("default"))) int usv_debug_stamps(unsigned 
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_usv_stamps), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;
+}
+#endif
+
+#if USV_WGTIME
+extern "C" __attribute__((visibility("default"))) int usv_debug_wgtime(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_usv_wgtime), sizeof(unsigned long long) * 4 * n) != hipSuccess;
 }
 #endif
 
