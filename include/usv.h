@@ -29,6 +29,20 @@
  *   usv_generate_matching_list GenerateMatchingList, P/Main.cpp:403-426
  *                             (OpenCV matchShapes/contourArea restated; parity
  *                             unpinned -- OpenCV 3.0 is absent).
+ *   usv_rectify_params / _map initUndistortRectifyMap(..., CV_16SC2, ...),
+ *                             P/Main.cpp:352,357 (the
+ *                             reference rebuilds it every frame, we build once)
+ *   usv_remap_linear_u8,      remap(INTER_LINEAR, BORDER_CONSTANT, Scalar()),
+ *   usv_rectify_pair_u8       P/Main.cpp:353,358 (one launch for both cameras)
+ *   usv_bgr2hsv_hist_u8,      cvtColor BGR2HSV P/Main.cpp:919 + LightingCorrection
+ *   usv_equalize_hsv_bgr_gray_u8  (split/equalizeHist/merge/HSV2BGR,
+ *   usv_frame_prep_u8         P/Main.cpp:365-371) + cvtColor BGR2GRAY :921
+ *   usv_motion_mask_u8        ABSDiffSearch P/Main.cpp:299-312 (absdiff,
+ *                             threshold 40, MorphilogicalFilter :289-292)
+ *   usv_colour_mask_u8        ColourSearch P/Main.cpp:318-327 (two inRange,
+ *                             addWeighted, MorphilogicalFilter)
+ *   (OpenCV 3.0 u8 semantics restated in oracle/; parity unpinned against
+ *   OpenCV itself, which the image lacks -- SURVEY §8(c).)
  *
  * Status codes replace exceptions so the C++ layer (include/Match.hpp,
  * include/DistanceCalculator.hpp, include/Matching.hpp) can keep the
@@ -162,6 +176,65 @@ usv_status usv_moving_object_distance(int camera_side_left, int64_t ts_this,
 usv_status usv_coordinate_position(int camera_side_left, const double* dist, int n_dist,
                                    const float* this_pts, int n_this, int coordinate_display,
                                    double* xyz_out, int* n_out);
+
+/* ---- rectification ---- */
+
+/*
+ * HOST: the 25 doubles initUndistortRectifyMap derives from the calibration:
+ *   params = {inverse(P[:,0:3] * Rrect) (9, row-major), fx, fy, u0, v0,
+ *             k1 k2 p1 p2 k3 k4 k5 k6 s1 s2 s3 s4}
+ * K: 3x3 camera matrix; dist: n_dist in {0, 4, 5, 8, 12} coefficients;
+ * Rrect: 3x3 rectification rotation (NULL = identity); P: 3 x p_cols (3 or 4)
+ * projection / new camera matrix.  All row-major doubles.
+ */
+usv_status usv_rectify_params(const double* K, const double* dist, int n_dist, const double* Rrect,
+                              const double* P, int p_cols, double* params);
+
+/* DEVICE: the CV_16SC2 map1 (W x H x 2 int16) and CV_16UC1 map2 (W x H uint16,
+ * (v_frac << 5) | u_frac) for an output of W x H; params is a HOST array. */
+usv_status usv_rectify_map(const double* params, int W, int H, int16_t* map1, uint16_t* map2,
+                           void* stream);
+
+/* DEVICE: remap INTER_LINEAR / BORDER_CONSTANT(0) of a u8 image with cn = 1 or 3
+ * interleaved channels (sW x sH, spitch bytes) through dense maps of W x H. */
+usv_status usv_remap_linear_u8(const uint8_t* src, int sW, int sH, int spitch, int cn,
+                               const int16_t* map1, const uint16_t* map2, int W, int H,
+                               uint8_t* dst, int dpitch, void* stream);
+
+/* DEVICE: both cameras of a pair in one launch (same source / output geometry). */
+usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                               int cn, const int16_t* map1L, const uint16_t* map2L,
+                               const int16_t* map1R, const uint16_t* map2R, int W, int H,
+                               uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
+
+/* ---- per-frame colour chain and masks, all DEVICE ---- */
+
+/* BGR (3 B/px) -> HSV (H in [0,180)) and the 256-bin histogram of V into
+ * hist256 (cleared by this call on the stream). */
+usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
+                               int hsv_pitch, uint32_t* hist256, void* stream);
+
+/* equalizeHist of V from hist256 (V rewritten in hsv), then HSV2BGR into
+ * bgr_out and BGR2GRAY into gray.  W * H <= 2^24. */
+usv_status usv_equalize_hsv_bgr_gray_u8(const uint32_t* hist256, uint8_t* hsv, int W, int H,
+                                        int hsv_pitch, uint8_t* bgr_out, int bgr_pitch,
+                                        uint8_t* gray, int gray_pitch, void* stream);
+
+/* The two calls above: the reference's frame preparation after rectification. */
+usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
+                             int hsv_pitch, uint8_t* bgr_out, int bgr_pitch, uint8_t* gray,
+                             int gray_pitch, uint32_t* hist256, void* stream);
+
+/* |gray - prev| > thresh -> 255, then erode + dilate with the 5x5 ellipse
+ * (gray and prev share pitch). */
+usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch,
+                              int thresh, uint8_t* mask, int mask_pitch, void* stream);
+
+/* inRange(hsv, lo1, hi1) | inRange(hsv, lo2, hi2), then erode + dilate (5x5
+ * ellipse).  lo/hi: HOST arrays of 3 ints (H, S, V), inclusive. */
+usv_status usv_colour_mask_u8(const uint8_t* hsv, int W, int H, int pitch, const int* lo1,
+                              const int* hi1, const int* lo2, const int* hi2, uint8_t* mask,
+                              int mask_pitch, void* stream);
 
 #ifdef __cplusplus
 }

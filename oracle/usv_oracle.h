@@ -21,6 +21,12 @@
  *   - ResolveMatchList P/Main.cpp:432-477 and IDMatcher P/Main.cpp:483-499,
  *     pinned by the SURVEY.md §8(c) golden vectors (duplicate-emitting
  *     conflict pass; comma-operator Point3i).
+ *   - SURVEY.md §8(f) rows 1 and 3 (rectify_oracle.c, preproc_oracle.c):
+ *     initUndistortRectifyMap + remap (P/Main.cpp:351-359), BGR2HSV /
+ *     equalizeHist / HSV2BGR / BGR2GRAY (P/Main.cpp:365-371, 919-921), the
+ *     absdiff and inRange masks with their 5x5-ellipse erode + dilate
+ *     (P/Main.cpp:289-327).  OpenCV 3.0 semantics restated; parity unpinned
+ *     against OpenCV (absent), pinned by known-answer tests.
  *
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
  */
@@ -90,6 +96,32 @@ int usv_oracle_resolve_match_list(const usv_oracle_match* in, int n_in, usv_orac
 /* P/Main.cpp:483-499; out gets 3 ints per triple; returns the triple count. */
 int usv_oracle_id_matcher(const usv_oracle_match* cur, int n_cur,
                           const usv_oracle_match* old, int n_old, int* out_xyz);
+
+/* ---- §8(f) row 1: rectification (rectify_oracle.c) ---- */
+/* 3x3 inverse, cv::invert n == 3 path; returns 0 when singular. */
+int usv_oracle_invert3(const double* m, double* out);
+/* params (25 doubles): ir[9], fx, fy, u0, v0, k1 k2 p1 p2 k3 k4 k5 k6 s1 s2 s3 s4.
+ * K 3x3, dist n_dist in {0,4,5,8,12}, Rrect 3x3 (NULL = identity), P 3 x p_cols (3 or 4). */
+int usv_oracle_rectify_params(const double* K, const double* dist, int n_dist, const double* Rrect,
+                              const double* P, int p_cols, double* params);
+/* CV_16SC2 map1 (2 int16 per pixel) + CV_16UC1 map2, dense W x H. */
+int usv_oracle_rectify_map(const double* params, int W, int H, int16_t* map1, uint16_t* map2);
+/* remap INTER_LINEAR, BORDER_CONSTANT 0, u8 with cn interleaved channels. */
+int usv_oracle_remap_linear(const uint8_t* src, int sW, int sH, int spitch, int cn, const int16_t* map1,
+                            const uint16_t* map2, int W, int H, uint8_t* dst, int dpitch);
+
+/* ---- §8(f) row 3: colour chain and masks (preproc_oracle.c) ---- */
+void usv_oracle_bgr2hsv(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv, int hsv_pitch);
+void usv_oracle_equalize_lut(const uint32_t* hist, int total, uint8_t* lut);
+void usv_oracle_hsv2bgr(const uint8_t* hsv, int W, int H, int pitch, uint8_t* bgr, int bgr_pitch);
+void usv_oracle_bgr2gray(const uint8_t* bgr, int W, int H, int pitch, uint8_t* gray, int gray_pitch);
+/* bgr (pitch) -> dense hsv' (3W), bgr' (3W), gray (W). */
+int usv_oracle_frame_prep(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv_out, uint8_t* bgr_out,
+                          uint8_t* gray_out);
+int usv_oracle_motion_mask(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch, int thresh,
+                           uint8_t* mask, int mask_pitch);
+int usv_oracle_colour_mask(const uint8_t* hsv, int W, int H, int pitch, const int* lo1, const int* hi1,
+                           const int* lo2, const int* hi2, uint8_t* mask, int mask_pitch);
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,19 @@ _SIGS = {
     "usv_oracle_resolve_match_list": (c_int, [POINTER(oracle_match), c_int, POINTER(oracle_match)]),
     "usv_oracle_id_matcher": (c_int, [POINTER(oracle_match), c_int, POINTER(oracle_match), c_int,
                                       POINTER(c_int)]),
+    "usv_oracle_invert3": (c_int, [c_void_p, c_void_p]),
+    "usv_oracle_rectify_params": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "usv_oracle_rectify_map": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "usv_oracle_remap_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                        c_void_p, c_int]),
+    "usv_oracle_bgr2hsv": (None, [c_void_p, c_int, c_int, c_int, c_void_p, c_int]),
+    "usv_oracle_equalize_lut": (None, [c_void_p, c_int, c_void_p]),
+    "usv_oracle_hsv2bgr": (None, [c_void_p, c_int, c_int, c_int, c_void_p, c_int]),
+    "usv_oracle_bgr2gray": (None, [c_void_p, c_int, c_int, c_int, c_void_p, c_int]),
+    "usv_oracle_frame_prep": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "usv_oracle_motion_mask": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int]),
+    "usv_oracle_colour_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_int]),
 }
 
 _lib = None
@@ -68,4 +81,81 @@ def oracle_sad(L, R, D, w, metric="sad", variant="sliding", threads=0):
         rc = lib.usv_oracle_sad_sliding(L.ctypes.data, R.ctypes.data, W, H, W, D, w, m, out.ctypes.data,
                                         W, threads)
     assert rc == 0, rc
+    return out
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+def oracle_rectify_params(K, dist, R, P):
+    """25 doubles: ir[9], fx, fy, u0, v0, k1..s4 (rectify_oracle.c)."""
+    import numpy as np
+    lib = load_oracle()
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    P = np.ascontiguousarray(P, dtype=np.float64)
+    d = np.ascontiguousarray(dist if dist is not None else np.zeros(0), dtype=np.float64).ravel()
+    Rm = None if R is None else np.ascontiguousarray(R, dtype=np.float64)
+    out = np.zeros(25, dtype=np.float64)
+    rc = lib.usv_oracle_rectify_params(_p(K), _p(d) if d.size else None, int(d.size),
+                                       _p(Rm) if Rm is not None else None, _p(P), int(P.shape[1]), _p(out))
+    assert rc == 0, rc
+    return out
+
+
+def oracle_rectify_map(params, W, H):
+    import numpy as np
+    lib = load_oracle()
+    params = np.ascontiguousarray(params, dtype=np.float64)
+    m1 = np.zeros((H, W, 2), dtype=np.int16)
+    m2 = np.zeros((H, W), dtype=np.uint16)
+    assert lib.usv_oracle_rectify_map(_p(params), W, H, _p(m1), _p(m2)) == 0
+    return m1, m2
+
+
+def oracle_remap(src, m1, m2):
+    import numpy as np
+    lib = load_oracle()
+    src = np.ascontiguousarray(src)
+    sH, sW = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    H, W = m2.shape
+    out = np.zeros((H, W) if cn == 1 else (H, W, cn), dtype=np.uint8)
+    rc = lib.usv_oracle_remap_linear(_p(src), sW, sH, sW * cn, cn, _p(np.ascontiguousarray(m1)),
+                                     _p(np.ascontiguousarray(m2)), W, H, _p(out), W * cn)
+    assert rc == 0, rc
+    return out
+
+
+def oracle_frame_prep(bgr):
+    """(H, W, 3) u8 -> (hsv', bgr', gray)."""
+    import numpy as np
+    lib = load_oracle()
+    bgr = np.ascontiguousarray(bgr)
+    H, W = bgr.shape[:2]
+    hsv = np.zeros((H, W, 3), np.uint8)
+    out = np.zeros((H, W, 3), np.uint8)
+    gray = np.zeros((H, W), np.uint8)
+    assert lib.usv_oracle_frame_prep(_p(bgr), W, H, 3 * W, _p(hsv), _p(out), _p(gray)) == 0
+    return hsv, out, gray
+
+
+def oracle_motion_mask(gray, prev, thresh=40):
+    import numpy as np
+    lib = load_oracle()
+    gray, prev = np.ascontiguousarray(gray), np.ascontiguousarray(prev)
+    H, W = gray.shape
+    out = np.zeros((H, W), np.uint8)
+    assert lib.usv_oracle_motion_mask(_p(gray), _p(prev), W, H, W, thresh, _p(out), W) == 0
+    return out
+
+
+def oracle_colour_mask(hsv, lo1, hi1, lo2, hi2):
+    import numpy as np
+    lib = load_oracle()
+    hsv = np.ascontiguousarray(hsv)
+    H, W = hsv.shape[:2]
+    b = [np.ascontiguousarray(v, dtype=np.int32) for v in (lo1, hi1, lo2, hi2)]
+    out = np.zeros((H, W), np.uint8)
+    assert lib.usv_oracle_colour_mask(_p(hsv), W, H, 3 * W, *[_p(v) for v in b], _p(out), W) == 0
     return out

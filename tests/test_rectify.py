@@ -1,0 +1,196 @@
+"""Rectification: initUndistortRectifyMap CV_16SC2 + remap INTER_LINEAR.
+
+OpenCV 3.0 is absent and the reference has no fixtures for P/Main.cpp:351-359,
+so parity against OpenCV is UNPINNED.  The oracle restatement
+(oracle/rectify_oracle.c) is pinned here by known answers -- an identity
+calibration reproduces the source, an integer principal-point shift gives a
+shifted copy with zeros entering, a half-pixel shift gives the rounded mean of
+neighbours -- and by an independent numpy restatement of the fixed-point
+bilinear remap; the GPU kernels must equal the oracle bit for bit.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import load_oracle, oracle_rectify_map, oracle_rectify_params, oracle_remap
+from unsynchronized_stereo_vision_proj325_amd import _lib
+from unsynchronized_stereo_vision_proj325_amd.rectify import rectify_params, synthetic_calibration
+
+
+def numpy_remap(src, m1, m2):
+    """Independent restatement of remap INTER_LINEAR / BORDER_CONSTANT 0 (fixed point, 5+15 bits)."""
+    src = src if src.ndim == 3 else src[:, :, None]
+    sH, sW, cn = src.shape
+    sx = m1[..., 0].astype(np.int64)
+    sy = m1[..., 1].astype(np.int64)
+    ty = (m2 >> 5).astype(np.int64)
+    tx = (m2 & 31).astype(np.int64)
+    w = [(32 - ty) * (32 - tx) * 32, (32 - ty) * tx * 32, ty * (32 - tx) * 32, ty * tx * 32]
+    acc = np.zeros(sx.shape + (cn,), dtype=np.int64)
+    for k, (dy, dx) in enumerate([(0, 0), (0, 1), (1, 0), (1, 1)]):
+        yy, xx = sy + dy, sx + dx
+        ok = (yy >= 0) & (yy < sH) & (xx >= 0) & (xx < sW)
+        v = src[np.clip(yy, 0, sH - 1), np.clip(xx, 0, sW - 1)].astype(np.int64)
+        acc += np.where(ok[..., None], v, 0) * w[k][..., None]
+    out = np.clip((acc + (1 << 14)) >> 15, 0, 255)
+    outside = (sx >= sW) | (sx + 1 < 0) | (sy >= sH) | (sy + 1 < 0)
+    out[outside] = 0
+    out = out.astype(np.uint8)
+    return out[..., 0] if cn == 1 else out
+
+
+def pinhole(f, cx, cy):
+    return np.array([[f, 0, cx], [0, f, cy], [0, 0, 1.0]])
+
+
+def test_identity_calibration_reproduces_source():
+    K = pinhole(500.0, 320.0, 240.0)
+    m1, m2 = oracle_rectify_map(oracle_rectify_params(K, None, None, K), 64, 48)
+    ys, xs = np.mgrid[0:48, 0:64]
+    assert np.array_equal(m1[..., 0], xs) and np.array_equal(m1[..., 1], ys) and not m2.any()
+    src = np.random.default_rng(0).integers(0, 256, (48, 64, 3), dtype=np.uint8)
+    assert np.array_equal(oracle_remap(src, m1, m2), src)
+
+
+@pytest.mark.parametrize("shift", [3, -5])
+def test_integer_principal_point_shift(shift):
+    K = pinhole(500.0, 320.0, 240.0)
+    P = np.hstack([pinhole(500.0, 320.0 + shift, 240.0), np.zeros((3, 1))])
+    m1, m2 = oracle_rectify_map(oracle_rectify_params(K, None, None, P), 40, 20)
+    src = np.random.default_rng(1).integers(1, 256, (20, 40), dtype=np.uint8)
+    out = oracle_remap(src, m1, m2)
+    exp = np.zeros_like(src)
+    if shift > 0:
+        exp[:, shift:] = src[:, :-shift]
+    else:
+        exp[:, :shift] = src[:, -shift:]
+    assert np.array_equal(out, exp)
+
+
+def test_half_pixel_shift_rounds_the_mean():
+    K = pinhole(400.0, 100.0, 50.0)
+    P = pinhole(400.0, 100.5, 50.0)
+    m1, m2 = oracle_rectify_map(oracle_rectify_params(K, None, None, P), 30, 10)
+    assert ((m2 & 31) == 16).all() and ((m2 >> 5) == 0).all()
+    src = np.random.default_rng(2).integers(0, 256, (10, 30), dtype=np.uint8)
+    out = oracle_remap(src, m1, m2).astype(int)
+    s = src.astype(int)
+    assert np.array_equal(out[:, 1:], (s[:, :-1] + s[:, 1:] + 1) >> 1)
+    assert np.array_equal(out[:, 0], (s[:, 0] + 1) >> 1)  # left tap outside the image reads 0
+
+
+@pytest.mark.parametrize("cn", [1, 3])
+def test_oracle_remap_matches_numpy_restatement(cn):
+    rng = np.random.default_rng(3 + cn)
+    sH, sW, H, W = 37, 53, 29, 41
+    src = rng.integers(0, 256, (sH, sW) if cn == 1 else (sH, sW, cn), dtype=np.uint8)
+    m1 = np.stack([rng.integers(-4, sW + 3, (H, W)), rng.integers(-4, sH + 3, (H, W))], -1).astype(np.int16)
+    m2 = rng.integers(0, 1024, (H, W)).astype(np.uint16)
+    assert np.array_equal(oracle_remap(src, m1, m2), numpy_remap(src, m1, m2))
+
+
+def test_invert3_against_numpy():
+    lib = load_oracle()
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        m = rng.normal(size=(3, 3))
+        out = np.zeros(9)
+        assert lib.usv_oracle_invert3(m.ctypes.data, out.ctypes.data) == 1
+        np.testing.assert_allclose(out.reshape(3, 3), np.linalg.inv(m), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("ndist", [0, 4, 5, 8, 12])
+def test_library_params_equal_oracle(ndist):
+    """usv_rectify_params (host code of libusv.so; no GPU needed) == the oracle, bit for bit."""
+    rng = np.random.default_rng(10 + ndist)
+    (K, dist, R, P), _ = synthetic_calibration(640, 480, seed=ndist)
+    d = rng.uniform(-0.2, 0.2, ndist)
+    got = rectify_params(K, d, R, P)
+    ref = oracle_rectify_params(K, d, R, P)
+    assert np.array_equal(got, ref)
+
+
+def test_library_rejects_bad_calibration():
+    lib = _lib.load()
+    out = np.zeros(25)
+    K = pinhole(1.0, 0.0, 0.0)
+    sing = np.zeros((3, 4))
+    assert lib.usv_rectify_params(K.ctypes.data, None, 0, None, sing.ctypes.data, 4, out.ctypes.data) == \
+        _lib.USV_ERR_INVALID_ARG
+    d = np.zeros(6)
+    assert lib.usv_rectify_params(K.ctypes.data, d.ctypes.data, 6, None, K.ctypes.data, 3, out.ctypes.data) == \
+        _lib.USV_ERR_INVALID_ARG
+
+
+# ---------------------------------------------------------------- GPU parity
+def _dev_maps(gpu, K, dist, R, P, W, H):
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier
+    return Rectifier(K, dist, R, P, (W, H), device=gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,seed,ndist", [(640, 480, 0, 5), (1920, 1080, 1, 5), (333, 97, 2, 8),
+                                            (1000, 700, 3, 12), (64, 64, 4, 0)])
+def test_gpu_map_bitexact(gpu, W, H, seed, ndist):
+    (K, dist, R, P), _ = synthetic_calibration(W, H, seed=seed)
+    d = np.resize(dist, ndist) if ndist else None
+    rect = _dev_maps(gpu, K, d, R, P, W, H)
+    m1, m2 = rect.maps_numpy()
+    r1, r2 = oracle_rectify_map(oracle_rectify_params(K, d, R, P), W, H)
+    assert np.array_equal(m1, r1), int((m1 != r1).sum())
+    assert np.array_equal(m2, r2), int((m2 != r2).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cn", [1, 3])
+@pytest.mark.parametrize("W,H", [(640, 480), (1920, 1080), (97, 41), (3, 2)])
+def test_gpu_remap_bitexact(gpu, cn, W, H):
+    import torch
+    (K, dist, R, P), _ = synthetic_calibration(W, H, seed=W + cn)
+    rect = _dev_maps(gpu, K, dist, R, P, W, H)
+    rng = np.random.default_rng(W * H + cn)
+    src = rng.integers(0, 256, (H, W) if cn == 1 else (H, W, cn), dtype=np.uint8)
+    got = rect(torch.from_numpy(src).to(gpu)).cpu().numpy()
+    m1, m2 = rect.maps_numpy()
+    assert np.array_equal(got, oracle_remap(src, m1, m2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cn", [1, 3])
+def test_gpu_remap_wild_maps_and_pitched_output(gpu, cn):
+    """Maps pointing far outside the source (negative, past the border), odd widths, pitched dst."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(77 + cn)
+    sH, sW, H, W = 50, 70, 33, 45
+    src = rng.integers(0, 256, (sH, sW) if cn == 1 else (sH, sW, cn), dtype=np.uint8)
+    m1 = np.stack([rng.integers(-300, 400, (H, W)), rng.integers(-300, 400, (H, W))], -1).astype(np.int16)
+    m1[::3] = np.stack([rng.integers(-2, sW + 1, (H, W)), rng.integers(-2, sH + 1, (H, W))], -1)[::3]
+    m2 = rng.integers(0, 1024, (H, W)).astype(np.uint16)
+    d_src = torch.from_numpy(src).to(gpu)
+    d_m1 = torch.from_numpy(m1).to(gpu)
+    d_m2 = torch.from_numpy(m2.view(np.int16)).to(gpu)
+    big = torch.zeros((H, (W + 13) * cn), dtype=torch.uint8, device=gpu)
+    lib = _lib.load()
+    st = lib.usv_remap_linear_u8(d_src.data_ptr(), sW, sH, sW * cn, cn, d_m1.data_ptr(), d_m2.data_ptr(), W, H,
+                                 big.data_ptr(), big.stride(0), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == _lib.USV_OK
+    got = big[:, :W * cn].cpu().numpy()
+    ref = oracle_remap(src, m1, m2).reshape(H, W * cn)
+    assert np.array_equal(got, ref)
+    assert not big[:, W * cn:].any()  # nothing written past the row
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cn", [1, 3])
+def test_gpu_rectify_pair_equals_two_remaps(gpu, cn):
+    import torch
+    from unsynchronized_stereo_vision_proj325_amd.rectify import rectify_pair
+    W, H = 640, 480
+    (cl, cr) = synthetic_calibration(W, H, seed=9)
+    rl, rr = _dev_maps(gpu, *cl, W, H), _dev_maps(gpu, *cr, W, H)
+    rng = np.random.default_rng(cn)
+    shape = (H, W) if cn == 1 else (H, W, cn)
+    sl = torch.from_numpy(rng.integers(0, 256, shape, dtype=np.uint8)).to(gpu)
+    sr = torch.from_numpy(rng.integers(0, 256, shape, dtype=np.uint8)).to(gpu)
+    ol, orr = rectify_pair(rl, rr, sl, sr)
+    assert torch.equal(ol, rl(sl)) and torch.equal(orr, rr(sr))

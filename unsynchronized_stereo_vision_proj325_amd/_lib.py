@@ -73,6 +73,20 @@ SIGNATURES = {
                                            POINTER(c_double), POINTER(c_float), POINTER(c_int)]),
     "usv_coordinate_position": (c_int, [c_int, POINTER(c_double), c_int, POINTER(c_float), c_int, c_int,
                                         POINTER(c_double), POINTER(c_int)]),
+    "usv_rectify_params": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "usv_rectify_map": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "usv_remap_linear_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                    c_void_p, c_int, c_void_p]),
+    "usv_rectify_pair_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "usv_bgr2hsv_hist_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "usv_equalize_hsv_bgr_gray_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                             c_void_p, c_int, c_void_p]),
+    "usv_frame_prep_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                  c_int, c_void_p, c_void_p]),
+    "usv_motion_mask_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "usv_colour_mask_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

@@ -1,0 +1,250 @@
+// usv_rectify.hip -- stereo rectification on gfx950.
+//
+// The reference rebuilds the OpenCV rectification map for every frame of
+// both cameras and remaps with it (P/Main.cpp:351-359: initUndistortRectifyMap
+// CV_16SC2 + remap INTER_LINEAR, BORDER_CONSTANT 0); the calibration struct is
+// passed by value, so the map never survives a call.  Here the map is built
+// once per calibration on the device (rectify_map_kernel, f64, the OpenCV
+// column recurrence replayed exactly) and every frame is one HBM-bound gather
+// (remap_kernel): 6 B of map + the output bytes per pixel, the source served
+// from L2.  Both cameras go in one launch (grid z).  Semantics restated in
+// oracle/rectify_oracle.c; the two agree bit for bit (tests/test_rectify.py).
+#include <climits>
+
+#include "usv.h"
+#include "usv_kernels.hpp"
+
+namespace usv {
+namespace {
+
+struct RectParams {
+    double ir[9];
+    double fx, fy, u0, v0;
+    double k[12];  // k1 k2 p1 p2 k3 k4 k5 k6 s1 s2 s3 s4
+};
+
+__device__ __forceinline__ int sat_round(double v) {
+    if (!(v > -2147483648.0)) return INT_MIN;
+    if (v >= 2147483647.0) return INT_MAX;
+    return __double2int_rn(v);
+}
+
+constexpr int kMapChunk = 32;  // columns per thread
+
+// One thread per (row, chunk of kMapChunk columns).  OpenCV walks a row with
+// _x += ir[0] (etc.) per column, so the thread first replays that recurrence
+// from column 0 to its chunk: three dependent f64 adds per skipped column, the
+// same rounding sequence as the sequential loop.
+__global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, int H, int16_t* __restrict__ map1,
+                                                         uint16_t* __restrict__ map2) {
+    const int i = blockIdx.y;
+    const int j0 = (blockIdx.x * 64 + threadIdx.x) * kMapChunk;
+    if (i >= H || j0 >= W) return;
+    const double* ir = p.ir;
+    double _x = i * ir[1] + ir[2], _y = i * ir[4] + ir[5], _w = i * ir[7] + ir[8];
+    for (int j = 0; j < j0; ++j) {
+        _x += ir[0];
+        _y += ir[3];
+        _w += ir[6];
+    }
+    const double k1 = p.k[0], k2 = p.k[1], p1 = p.k[2], p2 = p.k[3], k3 = p.k[4], k4 = p.k[5];
+    const double k5 = p.k[6], k6 = p.k[7], s1 = p.k[8], s2 = p.k[9], s3 = p.k[10], s4 = p.k[11];
+    const int j1 = min(W, j0 + kMapChunk);
+    int16_t* m1 = map1 + (size_t)i * W * 2;
+    uint16_t* m2 = map2 + (size_t)i * W;
+    for (int j = j0; j < j1; ++j, _x += ir[0], _y += ir[3], _w += ir[6]) {
+        const double w = 1. / _w, x = _x * w, y = _y * w;
+        const double x2 = x * x, y2 = y * y;
+        const double r2 = x2 + y2, _2xy = 2 * x * y;
+        const double kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2);
+        const double u = p.fx * (x * kr + p1 * _2xy + p2 * (r2 + 2 * x2) + s1 * r2 + s2 * r2 * r2) + p.u0;
+        const double v = p.fy * (y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy + s3 * r2 + s4 * r2 * r2) + p.v0;
+        const int iu = sat_round(u * 32), iv = sat_round(v * 32);
+        m1[j * 2] = (int16_t)(iu >> 5);
+        m1[j * 2 + 1] = (int16_t)(iv >> 5);
+        m2[j] = (uint16_t)((iv & 31) * 32 + (iu & 31));
+    }
+}
+
+struct RemapJob {
+    const uint8_t* src;
+    int spitch;
+    const int16_t* map1;
+    const uint16_t* map2;
+    uint8_t* dst;
+    int dpitch;
+};
+
+// 4 output pixels per thread: the map arrives as one 16-B and one 8-B load
+// (when the rows are 4-pixel aligned), the four taps of each pixel come from
+// L2 / L1 (a rectification map moves a pixel by a few source columns), the
+// result leaves as one 4-B (gray) or three 4-B (BGR) stores.
+template <int CN>
+__global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
+                                                    int vec_map, int vec_dst) {
+    const RemapJob& j = blockIdx.z ? j1 : j0;
+    const int y = blockIdx.y;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (x0 >= W || y >= H) return;
+    const int n = min(4, W - x0);
+    const size_t mrow = (size_t)y * W + x0;
+    int mx[4], my[4], mf[4];
+    if (vec_map && n == 4) {
+        const int4 a = *reinterpret_cast<const int4*>(j.map1 + 2 * mrow);
+        const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
+        const int w4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mx[q] = (int)(int16_t)(w4[q] & 0xFFFF);
+            my[q] = (int)(int16_t)((unsigned)w4[q] >> 16);
+        }
+        mf[0] = f.x & 0xFFFF;
+        mf[1] = f.x >> 16;
+        mf[2] = f.y & 0xFFFF;
+        mf[3] = f.y >> 16;
+    } else {
+        for (int q = 0; q < 4; ++q) {
+            const int qq = q < n ? q : 0;
+            mx[q] = j.map1[2 * (mrow + qq)];
+            my[q] = j.map1[2 * (mrow + qq) + 1];
+            mf[q] = j.map2[mrow + qq];
+        }
+    }
+    uint8_t out[4 * CN];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int sx = mx[q], sy = my[q];
+        const int ty = mf[q] >> 5, tx = mf[q] & 31;
+        const int w0 = (32 - ty) * (32 - tx) * 32, w1 = (32 - ty) * tx * 32;
+        const int w2 = ty * (32 - tx) * 32, w3 = ty * tx * 32;
+        if (sx >= sW || sx + 1 < 0 || sy >= sH || sy + 1 < 0) {
+#pragma unroll
+            for (int k = 0; k < CN; ++k) out[q * CN + k] = 0;
+            continue;
+        }
+        const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
+        const uint8_t* r0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
+        const uint8_t* r1 = r0 + j.spitch;
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const int v0 = (x0ok && y0ok) ? r0[k] : 0;
+            const int v1 = (x1ok && y0ok) ? r0[CN + k] : 0;
+            const int v2 = (x0ok && y1ok) ? r1[k] : 0;
+            const int v3 = (x1ok && y1ok) ? r1[CN + k] : 0;
+            const int t = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
+            out[q * CN + k] = (uint8_t)min(max(t, 0), 255);
+        }
+    }
+    uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
+    if (vec_dst && n == 4) {
+#pragma unroll
+        for (int w = 0; w < CN; ++w)
+            reinterpret_cast<uint32_t*>(d)[w] = (uint32_t)out[4 * w] | ((uint32_t)out[4 * w + 1] << 8) |
+                                                ((uint32_t)out[4 * w + 2] << 16) | ((uint32_t)out[4 * w + 3] << 24);
+    } else {
+        for (int b = 0; b < n * CN; ++b) d[b] = out[b];
+    }
+}
+
+bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn, int sW, int sH, int W, int H,
+                        hipStream_t s) {
+    bool vec_map = (W % 4) == 0, vec_dst = true;
+    for (int i = 0; i < n_jobs; ++i) {
+        const RemapJob& j = i ? b : a;
+        vec_map = vec_map && aligned(j.map1, 16) && aligned(j.map2, 8);
+        vec_dst = vec_dst && aligned(j.dst, 4) && (j.dpitch % 4) == 0;
+    }
+    dim3 grid((unsigned)((W + 1023) / 1024), (unsigned)H, (unsigned)n_jobs), block(256);
+    if (cn == 1)
+        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst);
+    else if (cn == 3)
+        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst);
+    else
+        return USV_ERR_UNSUPPORTED;
+    return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
+}
+
+bool job_ok(const RemapJob& j, int cn, int sW, int W) {
+    return j.src && j.map1 && j.map2 && j.dst && j.spitch >= sW * cn && j.dpitch >= W * cn;
+}
+
+}  // namespace
+}  // namespace usv
+
+extern "C" {
+
+usv_status usv_rectify_params(const double* K, const double* dist, int n_dist, const double* Rrect,
+                              const double* P, int p_cols, double* params) {
+    if (!K || !P || !params || (p_cols != 3 && p_cols != 4)) return USV_ERR_INVALID_ARG;
+    if (!(n_dist == 0 || n_dist == 4 || n_dist == 5 || n_dist == 8 || n_dist == 12) || (n_dist && !dist))
+        return USV_ERR_INVALID_ARG;
+    double Rm[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (Rrect)
+        for (int i = 0; i < 9; ++i) Rm[i] = Rrect[i];
+    // Ar.colRange(0,3) * R, then its inverse by adjugate / determinant (cv::invert, n <= 3)
+    double A[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            A[i * 3 + j] = P[i * p_cols] * Rm[j] + P[i * p_cols + 1] * Rm[3 + j] + P[i * p_cols + 2] * Rm[6 + j];
+    auto m = [&](int i, int j) { return A[i * 3 + j]; };
+    double det = m(0, 0) * (m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1)) - m(0, 1) * (m(1, 0) * m(2, 2) - m(1, 2) * m(2, 0)) +
+                 m(0, 2) * (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0));
+    if (det == 0.) return USV_ERR_INVALID_ARG;
+    det = 1. / det;
+    params[0] = (m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1)) * det;
+    params[1] = (m(0, 2) * m(2, 1) - m(0, 1) * m(2, 2)) * det;
+    params[2] = (m(0, 1) * m(1, 2) - m(0, 2) * m(1, 1)) * det;
+    params[3] = (m(1, 2) * m(2, 0) - m(1, 0) * m(2, 2)) * det;
+    params[4] = (m(0, 0) * m(2, 2) - m(0, 2) * m(2, 0)) * det;
+    params[5] = (m(0, 2) * m(1, 0) - m(0, 0) * m(1, 2)) * det;
+    params[6] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * det;
+    params[7] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * det;
+    params[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * det;
+    params[9] = K[0];
+    params[10] = K[4];
+    params[11] = K[2];
+    params[12] = K[5];
+    for (int i = 0; i < 12; ++i) params[13 + i] = i < n_dist ? dist[i] : 0.;
+    return USV_OK;
+}
+
+usv_status usv_rectify_map(const double* params, int W, int H, int16_t* map1, uint16_t* map2, void* stream) {
+    if (!params || !map1 || !map2 || W <= 0 || H <= 0 || W > 32767 || H > 32767) return USV_ERR_INVALID_ARG;
+    usv::RectParams p;
+    for (int i = 0; i < 9; ++i) p.ir[i] = params[i];
+    p.fx = params[9];
+    p.fy = params[10];
+    p.u0 = params[11];
+    p.v0 = params[12];
+    for (int i = 0; i < 12; ++i) p.k[i] = params[13 + i];
+    const int chunks = (W + usv::kMapChunk - 1) / usv::kMapChunk;
+    dim3 grid((unsigned)((chunks + 63) / 64), (unsigned)H), block(64);
+    hipLaunchKernelGGL(usv::rectify_map_kernel, grid, block, 0, static_cast<hipStream_t>(stream), p, W, H, map1,
+                       map2);
+    return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
+}
+
+usv_status usv_remap_linear_u8(const uint8_t* src, int sW, int sH, int spitch, int cn, const int16_t* map1,
+                               const uint16_t* map2, int W, int H, uint8_t* dst, int dpitch, void* stream) {
+    if (sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    const usv::RemapJob j{src, spitch, map1, map2, dst, dpitch};
+    if (!usv::job_ok(j, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    return usv::launch_remap(j, j, 1, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch, int cn,
+                               const int16_t* map1L, const uint16_t* map2L, const int16_t* map1R,
+                               const uint16_t* map2R, int W, int H, uint8_t* dstL, uint8_t* dstR, int dpitch,
+                               void* stream) {
+    if (sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    const usv::RemapJob a{srcL, spitch, map1L, map2L, dstL, dpitch};
+    const usv::RemapJob b{srcR, spitch, map1R, map2R, dstR, dpitch};
+    if (!usv::job_ok(a, cn, sW, W) || !usv::job_ok(b, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    return usv::launch_remap(a, b, 2, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

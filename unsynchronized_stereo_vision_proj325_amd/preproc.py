@@ -1,0 +1,119 @@
+"""Per-frame colour chain and masks on the GPU.
+
+Mirrors what the reference does to every rectified frame (P/Main.cpp:915-921
+and the search helpers it calls), with the reference's function names where it
+has them:
+
+  ``frame_prep``        cvtColor BGR2HSV -> LightingCorrection (split /
+                        equalizeHist(V) / merge / HSV2BGR) -> cvtColor BGR2GRAY
+                        (P/Main.cpp:919-921, 365-371); returns (hsv', bgr', gray)
+  ``ABSDiffSearch``     absdiff with the previous gray frame, threshold 40,
+                        MorphilogicalFilter (P/Main.cpp:299-312, 289-292)
+  ``ColourSearch``      two inRange + addWeighted + MorphilogicalFilter
+                        (P/Main.cpp:318-327)
+
+All compute is in libusv.so (csrc/usv_preproc.hip); inputs must be uint8 GPU
+tensors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import _stream
+
+
+def _u8(t: torch.Tensor, name: str, channels: int) -> None:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.uint8:
+        raise ValueError(f"{name} must be a uint8 CUDA (HIP) tensor; there is no CPU path")
+    want = 2 if channels == 1 else 3
+    if t.dim() != want or (channels > 1 and t.shape[2] != channels) or t.stride(-1) != 1:
+        raise ValueError(f"{name} must be {'(H, W)' if channels == 1 else f'(H, W, {channels})'} contiguous rows")
+    if channels > 1 and t.stride(1) != channels:
+        raise ValueError(f"{name} must hold interleaved channels")
+
+
+class FramePrep:
+    """Reusable device scratch (the 256-bin histogram) for frame_prep on one device."""
+
+    def __init__(self, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.hist = torch.zeros(256, dtype=torch.int32, device=dev)
+
+    def __call__(self, bgr: torch.Tensor, hsv: torch.Tensor | None = None, bgr_out: torch.Tensor | None = None,
+                 gray: torch.Tensor | None = None, stream=None):
+        _u8(bgr, "bgr", 3)
+        H, W = bgr.shape[:2]
+        hsv = torch.empty((H, W, 3), dtype=torch.uint8, device=bgr.device) if hsv is None else hsv
+        bgr_out = torch.empty((H, W, 3), dtype=torch.uint8, device=bgr.device) if bgr_out is None else bgr_out
+        gray = torch.empty((H, W), dtype=torch.uint8, device=bgr.device) if gray is None else gray
+        _u8(hsv, "hsv", 3)
+        _u8(bgr_out, "bgr_out", 3)
+        _u8(gray, "gray", 1)
+        lib = _lib.load()
+        with torch.cuda.device(bgr.device):
+            _lib.check("usv_frame_prep_u8", lib.usv_frame_prep_u8(
+                bgr.data_ptr(), W, H, bgr.stride(0), hsv.data_ptr(), hsv.stride(0), bgr_out.data_ptr(),
+                bgr_out.stride(0), gray.data_ptr(), gray.stride(0), self.hist.data_ptr(), _stream(stream)))
+        return hsv, bgr_out, gray
+
+
+def frame_prep(bgr: torch.Tensor, stream=None):
+    """(hsv', bgr', gray) of one rectified BGR frame; see FramePrep."""
+    return FramePrep(bgr.device)(bgr, stream=stream)
+
+
+def ABSDiffSearch(gray: torch.Tensor, prev: torch.Tensor | None, thresh: int = 40,
+                  out: torch.Tensor | None = None, stream=None):
+    """Motion mask of P/Main.cpp:299-312.  Returns (mask, next_prev): as in the
+    reference, an empty previous frame is replaced by the current one (first
+    call -> all-zero mask) and the current gray frame becomes the next prev."""
+    _u8(gray, "gray", 1)
+    if prev is None:
+        prev = gray
+    _u8(prev, "prev", 1)
+    if prev.shape != gray.shape or prev.stride() != gray.stride():
+        raise ValueError("prev must match gray's shape and strides")
+    H, W = gray.shape
+    out = torch.empty((H, W), dtype=torch.uint8, device=gray.device) if out is None else out
+    _u8(out, "out", 1)
+    lib = _lib.load()
+    with torch.cuda.device(gray.device):
+        _lib.check("usv_motion_mask_u8", lib.usv_motion_mask_u8(
+            gray.data_ptr(), prev.data_ptr(), W, H, gray.stride(0), int(thresh), out.data_ptr(), out.stride(0),
+            _stream(stream)))
+    return out, gray
+
+
+@dataclass
+class ColourSearchParameters:
+    """P/Main.cpp:159-165 (slider values): hue range 1 and 2, shared S and V ranges."""
+    iLowHue: int = 0
+    iLowSaturation: int = 0
+    iLowValue: int = 0
+    iHighHue: int = 179
+    iHighSaturation: int = 255
+    iHighValue: int = 255
+    iLowHue2: int = 0
+    iHighHue2: int = 0
+
+
+def ColourSearch(hsv: torch.Tensor, p: ColourSearchParameters, out: torch.Tensor | None = None, stream=None):
+    """Colour mask of P/Main.cpp:318-327 on an HSV frame."""
+    _u8(hsv, "hsv", 3)
+    H, W = hsv.shape[:2]
+    lo1 = np.array([p.iLowHue, p.iLowSaturation, p.iLowValue], dtype=np.int32)
+    hi1 = np.array([p.iHighHue, p.iHighSaturation, p.iHighValue], dtype=np.int32)
+    lo2 = np.array([p.iLowHue2, p.iLowSaturation, p.iLowValue], dtype=np.int32)
+    hi2 = np.array([p.iHighHue2, p.iHighSaturation, p.iHighValue], dtype=np.int32)
+    out = torch.empty((H, W), dtype=torch.uint8, device=hsv.device) if out is None else out
+    _u8(out, "out", 1)
+    lib = _lib.load()
+    with torch.cuda.device(hsv.device):
+        _lib.check("usv_colour_mask_u8", lib.usv_colour_mask_u8(
+            hsv.data_ptr(), W, H, hsv.stride(0), lo1.ctypes.data, hi1.ctypes.data, lo2.ctypes.data,
+            hi2.ctypes.data, out.data_ptr(), out.stride(0), _stream(stream)))
+    return out
