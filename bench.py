@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--gather", choices=["overlap", "sync", "none"], default="overlap")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget (N=1 only)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pipeline-steps", type=int, default=50,
+                   help="timed launches per pipeline leg (rectify / frame prep / mask); 0 = skip")
     return p.parse_args()
 
 
@@ -109,6 +111,58 @@ def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float):
         "sample": f"oracle sliding-window SAD, rows 0..{rows} of the {W}x{H} w={w} D={D} pair "
                   f"({rows * W} output pixels), best of {len(times)}",
     }
+
+
+def time_launches(fn, steps: int, stream) -> float:
+    """Average duration (us) of `fn()` over `steps` back-to-back launches, HIP events on `stream`.
+    A spin kernel ahead of the timed launches holds the stream while the host enqueues them all, so
+    the interval is GPU time, not Python launch overhead (these kernels run for a few us)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(int(steps * 4e5))  # ~0.2 ms of spinning per launch to enqueue
+    start.record(stream)
+    for _ in range(steps):
+        fn()
+    end.record(stream)
+    end.synchronize()
+    return start.elapsed_time(end) / steps * 1e3
+
+
+def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
+    """The per-frame stages around the block matcher, config C geometry,
+    synthetic BGR frames and calibration; each leg's roofline is HBM (algorithmic bytes / avg launch)."""
+    from unsynchronized_stereo_vision_proj325_amd.preproc import ABSDiffSearch, FramePrep
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
+
+    rng = np.random.default_rng(7)
+    cl, cr = synthetic_calibration(W, H, seed=1)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    out_l, out_r = torch.empty_like(src_l), torch.empty_like(src_r)
+    prep = FramePrep(dev)
+    hsv, bgr2, gray = torch.empty_like(src_l), torch.empty_like(src_l), torch.empty((H, W), dtype=torch.uint8,
+                                                                                   device=dev)
+    prev = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
+    mask = torch.empty_like(prev)
+    s = torch.cuda.current_stream()
+    px = W * H
+    legs = {
+        # 2 cameras x (map 4 + 2 B, source 3 B, output 3 B) per pixel
+        "rectify_pair_bgr": (lambda: rectify_pair(rl, rr, src_l, src_r, out_l, out_r), 2 * px * (6 + 3 + 3)),
+        # BGR2HSV+hist (3 in, 3 out) + equalize/HSV2BGR/gray (3 in, 3 + 3 + 1 out), one camera
+        "frame_prep": (lambda: prep(out_l, hsv, bgr2, gray), px * (3 + 3 + 3 + 7)),
+        # absdiff + threshold + erode + dilate: gray + prev in, mask out
+        "motion_mask": (lambda: ABSDiffSearch(gray, prev, out=mask), px * 3),
+    }
+    res = {}
+    for name, (fn, nbytes) in legs.items():
+        us = time_launches(fn, steps, s)
+        gbs = nbytes / (us * 1e-6) / 1e9
+        res[name] = {"us": us, "bytes": nbytes, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+    return res
 
 
 def main():
@@ -247,6 +301,11 @@ def main():
             "lane_ops_per_element": lane_ops / (pixels * D),
             "source": "SQ_INSTS_VALU per launch x 64 from profiles/counters.json, over this run's kernel time",
         }
+    if world == 1 and rank == 0 and a.pipeline_steps > 0:
+        rec["pipeline"] = {"workload": f"{W}x{H} BGR frames, synthetic calibration (5-term distortion)",
+                           "note": "per-frame stages around the matcher, SURVEY.md 8(f) rows 1 and 3; "
+                                   "HBM roofline per leg (algorithmic bytes / avg launch, HIP events)",
+                           **pipeline_legs(dev, W, H, a.pipeline_steps)}
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
         rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]
