@@ -209,21 +209,28 @@ usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW,
 
 /* ---- per-frame colour chain and masks, all DEVICE ---- */
 
-/* BGR (3 B/px) -> HSV (H in [0,180)) and the 256-bin histogram of V into
- * hist256 (cleared by this call on the stream). */
-usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
-                               int hsv_pitch, uint32_t* hist256, void* stream);
+/* Device workspace of the frame preparation: USV_FRAME_PREP_WORK_BYTES bytes
+ * (per parity, eight partial 256-bin u32 histograms of V), 4-byte aligned,
+ * ZERO-FILLED ONCE by the caller.  Consecutive frames alternate `parity` (0, 1, 0, ...): a call fills
+ * histogram `parity` and clears the other one for the next frame.  One
+ * workspace per stream in flight. */
+#define USV_FRAME_PREP_WORK_BYTES (2 * 8 * 256 * 4)
 
-/* equalizeHist of V from hist256 (V rewritten in hsv), then HSV2BGR into
- * bgr_out and BGR2GRAY into gray.  W * H <= 2^24. */
-usv_status usv_equalize_hsv_bgr_gray_u8(const uint32_t* hist256, uint8_t* hsv, int W, int H,
+/* BGR (3 B/px) -> HSV (H in [0,180)) and the 256-bin histogram of V into
+ * histogram `parity` of work.  W * H <= 2^24. */
+usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
+                               int hsv_pitch, void* work, int parity, void* stream);
+
+/* equalizeHist of V from histogram `parity` (V rewritten in hsv), then
+ * HSV2BGR into bgr_out and BGR2GRAY into gray. */
+usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* hsv, int W, int H,
                                         int hsv_pitch, uint8_t* bgr_out, int bgr_pitch,
                                         uint8_t* gray, int gray_pitch, void* stream);
 
 /* The two calls above: the reference's frame preparation after rectification. */
 usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
                              int hsv_pitch, uint8_t* bgr_out, int bgr_pitch, uint8_t* gray,
-                             int gray_pitch, uint32_t* hist256, void* stream);
+                             int gray_pitch, void* work, int parity, void* stream);
 
 /* |gray - prev| > thresh -> 255, then erode + dilate with the 5x5 ellipse
  * (gray and prev share pitch). */

@@ -5,12 +5,13 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
+SRC=${VARIANT_SRC:-usv_sad_fast}   # which kernel file the defines apply to
 C=unsynchronized_stereo_vision_proj325_amd/csrc
 make -s -C $C
 mkdir -p build_variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -ffp-contract=off "$@" \
-    -c $C/usv_sad_fast.hip -o build_variants/$name.fast.o
-objs=$(ls $C/build/*.o | grep -v usv_sad_fast.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.fast.o $objs
-rm -f build_variants/$name.fast.o
+    -c $C/$SRC.hip -o build_variants/$name.var.o
+objs=$(ls $C/build/*.o | grep -v "/$SRC.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.var.o $objs
+rm -f build_variants/$name.var.o
 echo built build_variants/$name.so

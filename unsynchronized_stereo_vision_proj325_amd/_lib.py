@@ -79,11 +79,11 @@ SIGNATURES = {
                                     c_void_p, c_int, c_void_p]),
     "usv_rectify_pair_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
-    "usv_bgr2hsv_hist_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
-    "usv_equalize_hsv_bgr_gray_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+    "usv_bgr2hsv_hist_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "usv_equalize_hsv_bgr_gray_u8": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                              c_void_p, c_int, c_void_p]),
     "usv_frame_prep_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
-                                  c_int, c_void_p, c_void_p]),
+                                  c_int, c_void_p, c_int, c_void_p]),
     "usv_motion_mask_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "usv_colour_mask_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_int, c_void_p]),

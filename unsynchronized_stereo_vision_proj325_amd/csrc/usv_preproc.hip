@@ -15,6 +15,8 @@
 // All three are HBM-bound byte streams: no MFMA, integer work
 // except the HSV2BGR float path, which follows OpenCV's float operations in
 // order (-ffp-contract=off).
+#include <algorithm>
+
 #include "usv.h"
 #include "usv_kernels.hpp"
 
@@ -22,6 +24,9 @@ namespace usv {
 namespace {
 
 constexpr int kHsvShift = 12;
+#ifndef USV_PREP_EXP
+#define USV_PREP_EXP 0  // timing experiments only (wrong histograms): 1 no global bin atomics, 2 no LDS atomics, 3 neither
+#endif
 
 __device__ __forceinline__ void bgr2hsv_px(int b, int g, int r, const int* sdiv, const int* hdiv, int& h, int& s,
                                            int& v) {
@@ -80,45 +85,133 @@ __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int&
     orr = round_u8(r * 255.f);
 }
 
-// One block per group of rows; per-block LDS histogram flushed with at most
-// 256 global atomics.  hist must be zero on entry (the C entry point clears it
-// on the same stream).
-__global__ __launch_bounds__(256) void hsv_hist_kernel(const uint8_t* __restrict__ bgr, int W, int H, int pitch,
-                                                       uint8_t* __restrict__ hsv, int hsv_pitch,
-                                                       uint32_t* __restrict__ hist) {
-    __shared__ int sdiv[256], hdiv[256];
-    __shared__ uint32_t lh[256];
-    hsv_tables(sdiv, hdiv);
-    lh[threadIdx.x] = 0;
-    __syncthreads();
-    for (int y = blockIdx.x; y < H; y += gridDim.x) {
-        const uint8_t* s = bgr + (size_t)y * pitch;
-        uint8_t* d = hsv + (size_t)y * hsv_pitch;
-        for (int x = threadIdx.x; x < W; x += 256) {
-            int h, sat, v;
-            bgr2hsv_px(s[3 * x], s[3 * x + 1], s[3 * x + 2], sdiv, hdiv, h, sat, v);
-            d[3 * x] = (uint8_t)h;
-            d[3 * x + 1] = (uint8_t)sat;
-            d[3 * x + 2] = (uint8_t)v;
-            atomicAdd(&lh[v], 1u);
-        }
+// Work buffer (include/usv.h USV_FRAME_PREP_WORK_BYTES): per parity (the
+// caller alternates it between frames) kHistCopies 256-bin histograms; block
+// b adds into copy b % kHistCopies so each bin address takes 1/kHistCopies of
+// the blocks' atomics (same-address atomics serialise at the memory side).
+constexpr int kWHist = 0, kHistCopies = 8, kParityWords = 256 * kHistCopies;
+
+// 4 interleaved BGR / HSV pixels = 12 bytes = one dwordx3 when the row and x
+// are 4-pixel aligned; byte access otherwise.
+struct Px4 { int c[12]; };
+__device__ __forceinline__ Px4 load_px4(const uint8_t* p, bool vec, int n) {
+    Px4 r;
+    if (vec) {
+        const uint3 w = *reinterpret_cast<const uint3*>(p);
+        const uint32_t ww[3] = {w.x, w.y, w.z};
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r.c[i] = (ww[i >> 2] >> (8 * (i & 3))) & 0xFF;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r.c[i] = i < 3 * n ? p[i] : 0;
     }
-    __syncthreads();
-    if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
+    return r;
+}
+__device__ __forceinline__ void store_px4(uint8_t* p, const Px4& v, bool vec, int n) {
+    if (vec) {
+        uint3 w;
+        w.x = v.c[0] | (v.c[1] << 8) | (v.c[2] << 16) | ((uint32_t)v.c[3] << 24);
+        w.y = v.c[4] | (v.c[5] << 8) | (v.c[6] << 16) | ((uint32_t)v.c[7] << 24);
+        w.z = v.c[8] | (v.c[9] << 8) | (v.c[10] << 16) | ((uint32_t)v.c[11] << 24);
+        *reinterpret_cast<uint3*>(p) = w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i)  // static indices: a dynamic one would put the array in scratch
+            if (i < 3 * n) p[i] = (uint8_t)v.c[i];
+    }
 }
 
-// equalizeHist's LUT, computed by every block from the 256-bin histogram
-// (inclusive scan in LDS; float scale and cvRound exactly as OpenCV), then
-// per pixel V' = LUT[V] (written back into hsv), HSV2BGR, BGR2GRAY.
-__global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restrict__ hist, int W, int H,
+// Pixels are processed as quads (4 interleaved pixels, one dwordx3) over the
+// whole image as one flat range: quad q -> row q / nq, column 4 (q % nq).  A
+// thread takes kU quads per sweep and issues all their loads before any
+// compute, and the grid is sized to one sweep (~4 waves per SIMD at 1080p): the
+// row-by-row form with a fixed 256-block grid ran latency-bound.  When W % 4 == 0 and the rows are 4-byte aligned
+// every full sweep is straight-line vector code; the rest take a byte path.
+constexpr int kU = 2;
+
+// for_each_quad(f): f(y, x, n, in) -> handles one quad; Load(y, x, n, vec) -> Px4.
+template <typename LoadF, typename BodyF>
+__device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF load, BodyF body) {
+    const int nq = (W + 3) >> 2;
+    const int Q = nq * H;  // W * H <= 2^24
+    const int stride = gridDim.x * 256 * kU;
+    for (int base = blockIdx.x * 256 * kU + threadIdx.x; base < Q; base += stride) {
+        if (vec4 && base + (kU - 1) * 256 < Q) {
+            int y[kU], x[kU];
+            Px4 in[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const unsigned q = (unsigned)(base + u * 256);
+                y[u] = (int)(q / (unsigned)nq);
+                x[u] = 4 * (int)(q - (unsigned)y[u] * (unsigned)nq);
+                in[u] = load(y[u], x[u], 4, true);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) body(y[u], x[u], 4, true, in[u]);
+        } else {
+            for (int u = 0; u < kU; ++u) {
+                const int q = base + u * 256;
+                if (q >= Q) break;
+                const int y = q / nq, x = 4 * (q - y * nq), n = min(4, W - x);
+                const bool v = vec4 && n == 4;
+                body(y, x, n, v, load(y, x, n, v));
+            }
+        }
+    }
+}
+
+// BGR2HSV + histogram of V.  Each block accumulates its histogram in LDS and
+// adds the occupied bins to histogram `parity` of the work buffer (no-return
+// atomics); block 0 also clears histogram 1 - parity, which the previous
+// frame used and the next one will fill.  (A single "last block" ticket to
+// build the LUT here cost ~40 us: 512 returning atomics on one address.)
+__global__ __launch_bounds__(256) void hsv_hist_kernel(const uint8_t* __restrict__ bgr, int W, int H, int pitch,
+                                                       uint8_t* __restrict__ hsv, int hsv_pitch,
+                                                       uint32_t* __restrict__ work, int parity, int vec) {
+    __shared__ int sdiv[256], hdiv[256];
+    __shared__ uint32_t lh[256];
+    const int t = threadIdx.x;
+    hsv_tables(sdiv, hdiv);
+    lh[t] = 0;
+    if (blockIdx.x == 0)
+        for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
+    __syncthreads();
+    const bool vec4 = vec && (W & 3) == 0;
+    for_each_quad(
+        W, H, vec4,
+        [&](int y, int x, int n, bool v) { return load_px4(bgr + (size_t)y * pitch + 3 * x, v, n); },
+        [&](int y, int x, int n, bool v, const Px4& in) {
+            Px4 out;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int h, sat, val;
+                bgr2hsv_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], sdiv, hdiv, h, sat, val);
+                out.c[3 * k] = h;
+                out.c[3 * k + 1] = sat;
+                out.c[3 * k + 2] = val;
+                if (!(USV_PREP_EXP & 2) && k < n) atomicAdd(&lh[val], 1u);
+            }
+            store_px4(hsv + (size_t)y * hsv_pitch + 3 * x, out, v, n);
+        });
+    __syncthreads();
+    if (!(USV_PREP_EXP & 1) && lh[t])
+        atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blockIdx.x % kHistCopies) + t], lh[t]);
+}
+
+// V' = LUT[V] written back into hsv, HSV2BGR, BGR2GRAY; kU quads per thread.
+__global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restrict__ work, int parity, int W, int H,
                                                        uint8_t* __restrict__ hsv, int hsv_pitch,
                                                        uint8_t* __restrict__ bgr, int bgr_pitch,
-                                                       uint8_t* __restrict__ gray, int gray_pitch) {
+                                                       uint8_t* __restrict__ gray, int gray_pitch, int vec) {
+    // equalizeHist's LUT from the complete histogram (every block builds it:
+    // an inclusive scan in LDS, then OpenCV's float scale and cvRound)
     __shared__ int scan[256];
     __shared__ int first;
     __shared__ uint8_t lut[256];
     const int t = threadIdx.x;
-    const int hv = (int)hist[t];
+    int hv = 0;
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c) hv += (int)work[kWHist + kParityWords * parity + 256 * c + t];
     if (t == 0) first = 256;
     scan[t] = hv;
     __syncthreads();
@@ -129,44 +222,55 @@ __global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restric
         scan[t] += add;
         __syncthreads();
     }
-    const int total = W * H;
-    const int i0 = first;
+    const int total = W * H, i0 = first;
     int lv = 0;
     if (i0 < 256) {
-        const int h0 = (int)hist[i0];
+        const int h0 = scan[i0] - (i0 ? scan[i0 - 1] : 0);
         if (h0 == total) {
             lv = t == i0 ? i0 : 0;  // dst.setTo(i0)
         } else if (t > i0) {
             const float scale = (256 - 1.f) / (total - h0);
-            const int sum = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
-            lv = min(max(__float2int_rn(sum * scale), 0), 255);
+            const int acc = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
+            lv = min(max(__float2int_rn(acc * scale), 0), 255);
         }
     }
     lut[t] = (uint8_t)lv;
     __syncthreads();
-    for (int y = blockIdx.x; y < H; y += gridDim.x) {
-        uint8_t* hs = hsv + (size_t)y * hsv_pitch;
-        uint8_t* bo = bgr + (size_t)y * bgr_pitch;
-        uint8_t* go = gray + (size_t)y * gray_pitch;
-        for (int x = threadIdx.x; x < W; x += 256) {
-            const int H8 = hs[3 * x], S8 = hs[3 * x + 1];
-            const int V8 = lut[hs[3 * x + 2]];
-            hs[3 * x + 2] = (uint8_t)V8;
-            int b, g, r;
-            hsv2bgr_px(H8, S8, V8, b, g, r);
-            bo[3 * x] = (uint8_t)b;
-            bo[3 * x + 1] = (uint8_t)g;
-            bo[3 * x + 2] = (uint8_t)r;
-            go[x] = (uint8_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14);
-        }
-    }
+    const bool vec4 = vec && (W & 3) == 0;
+    for_each_quad(
+        W, H, vec4,
+        [&](int y, int x, int n, bool v) { return load_px4(hsv + (size_t)y * hsv_pitch + 3 * x, v, n); },
+        [&](int y, int x, int n, bool v, Px4 in) {
+            Px4 o;
+            uint32_t g4 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
+                int b, g, r;
+                hsv2bgr_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], b, g, r);
+                o.c[3 * k] = b;
+                o.c[3 * k + 1] = g;
+                o.c[3 * k + 2] = r;
+                g4 |= (uint32_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14) << (8 * k);
+            }
+            store_px4(hsv + (size_t)y * hsv_pitch + 3 * x, in, v, n);
+            store_px4(bgr + (size_t)y * bgr_pitch + 3 * x, o, v, n);
+            uint8_t* go = gray + (size_t)y * gray_pitch + x;
+            if (v) *reinterpret_cast<uint32_t*>(go) = g4;
+            else for (int k = 0; k < n; ++k) go[k] = (uint8_t)(g4 >> (8 * k));
+        });
 }
 
 // ---- masks: threshold / inRange, then erode + dilate (5x5 ellipse) in one tile ----
-constexpr int kTW = 64, kTH = 16;            // output tile
-constexpr int kR = 2;                        // ellipse radius
-constexpr int kIW = kTW + 4 * kR, kIH = kTH + 4 * kR;  // thresholded input tile (two radii of halo)
-constexpr int kEW = kTW + 2 * kR, kEH = kTH + 2 * kR;  // eroded tile (one radius of halo)
+// Mask pixels are 0 or 255, so min / max are AND / OR and four pixels packed
+// in a u32 are processed at once; a shift by k pixels is v_alignbyte over the
+// neighbouring word.  The ellipse is rows -2 and +2 (centre only) and rows
+// -1..1 (five wide): E = T[-2] & T[+2] & h5(T[-1]) & h5(T[0]) & h5(T[+1]).
+constexpr int kTW = 64, kTH = 16;                        // output tile (pixels)
+constexpr int kR = 2;                                    // ellipse radius
+constexpr int kIH = kTH + 4 * kR, kIWW = (kTW + 8 * kR) / 4 + 0;  // input tile rows, words (4 px halo each side -> 80 px = 20 words)
+constexpr int kEH = kTH + 2 * kR, kEWW = kIWW - 2;      // eroded tile: 20 rows x 18 words (x0 - 4 .. x0 + 67)
+constexpr int kOWW = kTW / 4;                            // 16 output words per row
 
 struct MaskArgs {
     const uint8_t* a;  // gray (motion) or hsv (colour)
@@ -178,64 +282,104 @@ struct MaskArgs {
     int mask_pitch;
 };
 
-// the 17 taps of the 5x5 ellipse: rows -2 and 2 the centre column only
-template <bool ERODE>
-__device__ __forceinline__ int ellipse5(const uint8_t* t, int stride) {
-    // t points at the tap (dy, dx) = (0, 0)
-    int acc = t[-2 * stride];
-#define USV_TAP(o) acc = ERODE ? min(acc, (int)t[o]) : max(acc, (int)t[o])
-    USV_TAP(2 * stride);
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -2; dx <= 2; ++dx) USV_TAP(dy * stride + dx);
-#undef USV_TAP
-    return acc;
+__device__ __forceinline__ uint32_t shl_px(uint32_t lo, uint32_t hi, int k) {  // pixels x + k, k = 1..3
+    return __builtin_amdgcn_alignbyte(hi, lo, k);
+}
+template <bool AND>
+__device__ __forceinline__ uint32_t h5(const uint32_t* row, int j) {  // 5-wide AND / OR around word j
+    const uint32_t l = row[j - 1], c = row[j], r = row[j + 1];
+    const uint32_t m2 = __builtin_amdgcn_alignbyte(c, l, 2), m1 = __builtin_amdgcn_alignbyte(c, l, 3);
+    const uint32_t p1 = shl_px(c, r, 1), p2 = shl_px(c, r, 2);
+    return AND ? (c & m1 & m2 & p1 & p2) : (c | m1 | m2 | p1 | p2);
 }
 
 template <int MODE>  // 0: motion (absdiff > thresh), 1: colour (two inRange, saturating add)
-__global__ __launch_bounds__(256) void mask_kernel(MaskArgs m) {
-    __shared__ uint8_t T[kIH][kIW];
-    __shared__ uint8_t E[kEH][kEW];
-    const int X0 = blockIdx.x * kTW, Y0 = blockIdx.y * kTH;
-    for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
-        const int ty = i / kIW, tx = i - ty * kIW;
-        const int y = Y0 - 2 * kR + ty, x = X0 - 2 * kR + tx;
-        int v = 255;  // outside the image: never wins the erode min
-        if (y >= 0 && y < m.H && x >= 0 && x < m.W) {
-            if constexpr (MODE == 0) {
-                const int p = m.a[(size_t)y * m.pitch + x], q = m.b[(size_t)y * m.pitch + x];
-                v = (p > q ? p - q : q - p) > m.thresh ? 255 : 0;
-            } else {
-                const uint8_t* s = m.a + (size_t)y * m.pitch + 3 * x;
-                bool in1 = true, in2 = true;
+__device__ __forceinline__ int mask_px(const MaskArgs& m, int y, int x) {
+    if constexpr (MODE == 0) {
+        const int p = m.a[(size_t)y * m.pitch + x], q = m.b[(size_t)y * m.pitch + x];
+        return (p > q ? p - q : q - p) > m.thresh ? 255 : 0;
+    } else {
+        const uint8_t* s = m.a + (size_t)y * m.pitch + 3 * x;
+        bool in1 = true, in2 = true;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    in1 = in1 && s[c] >= m.lo1[c] && s[c] <= m.hi1[c];
-                    in2 = in2 && s[c] >= m.lo2[c] && s[c] <= m.hi2[c];
-                }
-                v = (in1 || in2) ? 255 : 0;
-            }
+        for (int c = 0; c < 3; ++c) {
+            in1 = in1 && s[c] >= m.lo1[c] && s[c] <= m.hi1[c];
+            in2 = in2 && s[c] >= m.lo2[c] && s[c] <= m.hi2[c];
         }
-        T[ty][tx] = (uint8_t)v;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kEH * kEW; i += 256) {
-        const int ey = i / kEW, ex = i - ey * kEW;
-        const int y = Y0 - kR + ey, x = X0 - kR + ex;
-        int v = 0;  // outside the image: never wins the dilate max
-        if (y >= 0 && y < m.H && x >= 0 && x < m.W) v = ellipse5<true>(&T[ey + kR][ex + kR], kIW);
-        E[ey][ex] = (uint8_t)v;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kTH * kTW; i += 256) {
-        const int oy = i / kTW, ox = i - oy * kTW;
-        const int y = Y0 + oy, x = X0 + ox;
-        if (y < m.H && x < m.W) m.mask[(size_t)y * m.mask_pitch + x] = (uint8_t)ellipse5<false>(&E[oy + kR][ox + kR], kEW);
+        return (in1 || in2) ? 255 : 0;
     }
 }
 
-int row_blocks(int H) { return H < 1024 ? H : 1024; }
+template <int MODE>
+__global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
+    __shared__ uint32_t T[kIH][kIWW];  // x0 - 8 .. x0 + 71
+    __shared__ uint32_t E[kEH][kEWW];  // word e covers x0 - 4 + 4e
+    const int X0 = blockIdx.x * kTW, Y0 = blockIdx.y * kTH;
+    // thresholded input, rows Y0-4 .. Y0+19, words x0-8 .. x0+71; outside the image = 255 (never wins the min)
+    for (int i = threadIdx.x; i < kIH * kIWW; i += 256) {
+        const int ty = i / kIWW, tw = i - ty * kIWW;
+        const int y = Y0 - 2 * kR + ty, x = X0 - 8 + 4 * tw;
+        uint32_t w = 0xFFFFFFFFu;
+        if (y >= 0 && y < m.H) {
+            if (MODE == 0 && vec && x >= 0 && x + 4 <= m.W) {
+                const uint32_t p = *reinterpret_cast<const uint32_t*>(m.a + (size_t)y * m.pitch + x);
+                const uint32_t q = *reinterpret_cast<const uint32_t*>(m.b + (size_t)y * m.pitch + x);
+                w = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int a = (p >> (8 * k)) & 0xFF, b = (q >> (8 * k)) & 0xFF;
+                    w |= (uint32_t)((a > b ? a - b : b - a) > m.thresh ? 255 : 0) << (8 * k);
+                }
+            } else {
+                w = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int xx = x + k;
+                    const int v = (xx >= 0 && xx < m.W) ? mask_px<MODE>(m, y, xx) : 255;
+                    w |= (uint32_t)v << (8 * k);
+                }
+            }
+        }
+        T[ty][tw] = w;
+    }
+    __syncthreads();
+    // erode, rows Y0-2 .. Y0+17, words x0-4 .. x0+67; outside the image = 0 (never wins the max)
+    for (int i = threadIdx.x; i < kEH * kEWW; i += 256) {
+        const int ey = i / kEWW, ew = i - ey * kEWW;
+        const int y = Y0 - kR + ey, x = X0 - 4 + 4 * ew;
+        const int tw = ew + 1, ty = ey + kR;
+        uint32_t e = T[ty - 2][tw] & T[ty + 2][tw] & h5<true>(T[ty - 1], tw) & h5<true>(T[ty], tw) &
+                     h5<true>(T[ty + 1], tw);
+        if (y < 0 || y >= m.H) e = 0;
+        else if (x < 0 || x + 4 > m.W) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x + k < 0 || x + k >= m.W) e &= ~(0xFFu << (8 * k));
+        }
+        E[ey][ew] = e;
+    }
+    __syncthreads();
+    // dilate, one output word (4 pixels) per thread
+    {
+        const int oy = threadIdx.x / kOWW, ow = threadIdx.x - oy * kOWW;
+        const int y = Y0 + oy, x = X0 + 4 * ow;
+        const int ew = ow + 1, ey = oy + kR;
+        const uint32_t d = E[ey - 2][ew] | E[ey + 2][ew] | h5<false>(E[ey - 1], ew) | h5<false>(E[ey], ew) |
+                           h5<false>(E[ey + 1], ew);
+        if (y < m.H && x < m.W) {
+            uint8_t* o = m.mask + (size_t)y * m.mask_pitch + x;
+            if (vec && x + 4 <= m.W) *reinterpret_cast<uint32_t*>(o) = d;
+            else for (int k = 0; k < 4 && x + k < m.W; ++k) o[k] = (uint8_t)(d >> (8 * k));
+        }
+    }
+}
+
+
+// one sweep of kU quads per thread, at most 4096 blocks (larger frames loop)
+int prep_blocks(int W, int H) {
+    const long long q = (long long)((W + 3) / 4) * H, per = 256LL * kU;
+    return (int)std::min<long long>(4096, std::max<long long>(1, (q + per - 1) / per));
+}
 
 usv_status st(hipError_t e) { return e == hipSuccess ? USV_OK : USV_ERR_HIP; }
 
@@ -244,34 +388,40 @@ usv_status st(hipError_t e) { return e == hipSuccess ? USV_OK : USV_ERR_HIP; }
 
 extern "C" {
 
+static bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+
 usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv, int hsv_pitch,
-                               uint32_t* hist256, void* stream) {
-    if (!bgr || !hsv || !hist256 || W <= 0 || H <= 0 || pitch < 3 * W || hsv_pitch < 3 * W)
+                               void* work, int parity, void* stream) {
+    if (!bgr || !hsv || !work || W <= 0 || H <= 0 || pitch < 3 * W || hsv_pitch < 3 * W ||
+        (long long)W * H > (1LL << 24) || !al4(work) || (parity != 0 && parity != 1))
         return USV_ERR_INVALID_ARG;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (hipMemsetAsync(hist256, 0, 256 * sizeof(uint32_t), s) != hipSuccess) return USV_ERR_HIP;
-    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(usv::row_blocks(H)), dim3(256), 0, s, bgr, W, H, pitch, hsv,
-                       hsv_pitch, hist256);
+    const int vec = al4(bgr) && al4(hsv) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
+    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(usv::prep_blocks(W, H)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       bgr, W, H, pitch, hsv, hsv_pitch, static_cast<uint32_t*>(work), parity, vec);
     return usv::st(hipGetLastError());
 }
 
-usv_status usv_equalize_hsv_bgr_gray_u8(const uint32_t* hist256, uint8_t* hsv, int W, int H, int hsv_pitch,
+usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* hsv, int W, int H, int hsv_pitch,
                                         uint8_t* bgr_out, int bgr_pitch, uint8_t* gray, int gray_pitch,
                                         void* stream) {
-    if (!hist256 || !hsv || !bgr_out || !gray || W <= 0 || H <= 0 || hsv_pitch < 3 * W || bgr_pitch < 3 * W ||
-        gray_pitch < W || (long long)W * H > (1LL << 24))
+    if (!work || !hsv || !bgr_out || !gray || W <= 0 || H <= 0 || hsv_pitch < 3 * W || bgr_pitch < 3 * W ||
+        gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) || (long long)W * H > (1LL << 24))
         return USV_ERR_INVALID_ARG;
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(usv::row_blocks(H)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       hist256, W, H, hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch);
+    const int vec = al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
+                    gray_pitch % 4 == 0;
+    hipLaunchKernelGGL(usv::equalize_kernel, dim3(usv::prep_blocks(W, H)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const uint32_t*>(work), parity, W, H, hsv, hsv_pitch, bgr_out, bgr_pitch, gray,
+                       gray_pitch, vec);
     return usv::st(hipGetLastError());
 }
 
 usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv, int hsv_pitch,
-                             uint8_t* bgr_out, int bgr_pitch, uint8_t* gray, int gray_pitch, uint32_t* hist256,
-                             void* stream) {
-    usv_status r = usv_bgr2hsv_hist_u8(bgr, W, H, pitch, hsv, hsv_pitch, hist256, stream);
+                             uint8_t* bgr_out, int bgr_pitch, uint8_t* gray, int gray_pitch, void* work,
+                             int parity, void* stream) {
+    usv_status r = usv_bgr2hsv_hist_u8(bgr, W, H, pitch, hsv, hsv_pitch, work, parity, stream);
     if (r != USV_OK) return r;
-    return usv_equalize_hsv_bgr_gray_u8(hist256, hsv, W, H, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch, stream);
+    return usv_equalize_hsv_bgr_gray_u8(work, parity, hsv, W, H, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
+                                        stream);
 }
 
 usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch, int thresh,
@@ -281,7 +431,8 @@ usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, i
     m.a = gray; m.b = prev; m.W = W; m.H = H; m.pitch = pitch; m.thresh = thresh;
     m.mask = mask; m.mask_pitch = mask_pitch;
     dim3 grid((unsigned)((W + usv::kTW - 1) / usv::kTW), (unsigned)((H + usv::kTH - 1) / usv::kTH));
-    hipLaunchKernelGGL(usv::mask_kernel<0>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m);
+    const int vec = al4(gray) && al4(prev) && al4(mask) && pitch % 4 == 0 && mask_pitch % 4 == 0;
+    hipLaunchKernelGGL(usv::mask_kernel<0>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m, vec);
     return usv::st(hipGetLastError());
 }
 
@@ -296,7 +447,8 @@ usv_status usv_colour_mask_u8(const uint8_t* hsv, int W, int H, int pitch, const
     }
     m.mask = mask; m.mask_pitch = mask_pitch;
     dim3 grid((unsigned)((W + usv::kTW - 1) / usv::kTW), (unsigned)((H + usv::kTH - 1) / usv::kTH));
-    hipLaunchKernelGGL(usv::mask_kernel<1>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m);
+    const int vec = al4(mask) && mask_pitch % 4 == 0;
+    hipLaunchKernelGGL(usv::mask_kernel<1>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m, vec);
     return usv::st(hipGetLastError());
 }
 

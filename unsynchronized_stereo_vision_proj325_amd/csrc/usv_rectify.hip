@@ -81,7 +81,7 @@ struct RemapJob {
 // result leaves as one 4-B (gray) or three 4-B (BGR) stores.
 template <int CN>
 __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
-                                                    int vec_map, int vec_dst) {
+                                                    int vec_map, int vec_dst, int vec_src) {
     const RemapJob& j = blockIdx.z ? j1 : j0;
     const int y = blockIdx.y;
     const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
@@ -125,6 +125,40 @@ __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, in
         const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
         const uint8_t* r0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
         const uint8_t* r1 = r0 + j.spitch;
+        // Interior: both taps of a row are 2*CN adjacent bytes; read the aligned
+        // dwords that hold them (2 for gray, 3 for BGR) and funnel-shift, unless
+        // the aligned read could run past the last source row.
+        constexpr int NW = CN == 1 ? 2 : 3;
+        const int boff = sx * CN, a = boff & ~3, o = boff & 3;
+        const bool interior = x0ok && x1ok && y0ok && y1ok && vec_src &&
+                              (sy + 1 < sH - 1 || a + 4 * NW <= j.spitch);
+        if (interior) {
+            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + (ptrdiff_t)sy * j.spitch + a);
+            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + j.spitch);
+            uint32_t u0[NW], u1[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                u0[i] = q0[i];
+                u1[i] = q1[i];
+            }
+            const uint32_t l0 = __builtin_amdgcn_alignbyte(u0[1], u0[0], o);  // tap bytes 0..3 of row 0
+            const uint32_t l1 = __builtin_amdgcn_alignbyte(u1[1], u1[0], o);
+            uint32_t h0 = 0, h1 = 0;
+            if constexpr (CN == 3) {
+                h0 = __builtin_amdgcn_alignbyte(u0[2], u0[1], o);  // tap bytes 4..7
+                h1 = __builtin_amdgcn_alignbyte(u1[2], u1[1], o);
+            }
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const int kb = CN + k;  // byte of the right tap
+                const int v0 = (l0 >> (8 * k)) & 0xFF, v2 = (l1 >> (8 * k)) & 0xFF;
+                const int v1 = kb < 4 ? (l0 >> (8 * kb)) & 0xFF : (h0 >> (8 * (kb - 4))) & 0xFF;
+                const int v3 = kb < 4 ? (l1 >> (8 * kb)) & 0xFF : (h1 >> (8 * (kb - 4))) & 0xFF;
+                const int t = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
+                out[q * CN + k] = (uint8_t)min(t, 255);
+            }
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
             const int v0 = (x0ok && y0ok) ? r0[k] : 0;
@@ -150,17 +184,18 @@ bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) %
 
 usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn, int sW, int sH, int W, int H,
                         hipStream_t s) {
-    bool vec_map = (W % 4) == 0, vec_dst = true;
+    bool vec_map = (W % 4) == 0, vec_dst = true, vec_src = true;
     for (int i = 0; i < n_jobs; ++i) {
         const RemapJob& j = i ? b : a;
         vec_map = vec_map && aligned(j.map1, 16) && aligned(j.map2, 8);
         vec_dst = vec_dst && aligned(j.dst, 4) && (j.dpitch % 4) == 0;
+        vec_src = vec_src && aligned(j.src, 4) && (j.spitch % 4) == 0;
     }
     dim3 grid((unsigned)((W + 1023) / 1024), (unsigned)H, (unsigned)n_jobs), block(256);
     if (cn == 1)
-        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst);
+        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst, (int)vec_src);
     else if (cn == 3)
-        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst);
+        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst, (int)vec_src);
     else
         return USV_ERR_UNSUPPORTED;
     return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;

@@ -37,11 +37,21 @@ def _u8(t: torch.Tensor, name: str, channels: int) -> None:
 
 
 class FramePrep:
-    """Reusable device scratch (the 256-bin histogram) for frame_prep on one device."""
+    """Reusable device workspace (two alternating 256-bin histograms; include/usv.h) for frame_prep on
+    one device.  One FramePrep per stream in flight."""
+
+    WORK_WORDS = 2 * 8 * 256  # USV_FRAME_PREP_WORK_BYTES / 4
 
     def __init__(self, device=None):
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.hist = torch.zeros(256, dtype=torch.int32, device=dev)
+        self.work = torch.zeros(self.WORK_WORDS, dtype=torch.int32, device=dev)
+        self.parity = 0
+
+    @property
+    def hist(self) -> torch.Tensor:
+        """The last frame's 256-bin histogram of V (equalizeHist's input)."""
+        p = 1 - self.parity
+        return self.work[2048 * p:2048 * (p + 1)].view(8, 256).sum(0)
 
     def __call__(self, bgr: torch.Tensor, hsv: torch.Tensor | None = None, bgr_out: torch.Tensor | None = None,
                  gray: torch.Tensor | None = None, stream=None):
@@ -57,7 +67,9 @@ class FramePrep:
         with torch.cuda.device(bgr.device):
             _lib.check("usv_frame_prep_u8", lib.usv_frame_prep_u8(
                 bgr.data_ptr(), W, H, bgr.stride(0), hsv.data_ptr(), hsv.stride(0), bgr_out.data_ptr(),
-                bgr_out.stride(0), gray.data_ptr(), gray.stride(0), self.hist.data_ptr(), _stream(stream)))
+                bgr_out.stride(0), gray.data_ptr(), gray.stride(0), self.work.data_ptr(), self.parity,
+                _stream(stream)))
+        self.parity ^= 1
         return hsv, bgr_out, gray
 
 
