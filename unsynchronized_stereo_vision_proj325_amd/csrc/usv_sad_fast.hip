@@ -69,6 +69,12 @@ constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_RED_LDS
 #define USV_RED_LDS 1  // argmin transpose through LDS (1) or permlane/DPP rounds (0)
 #endif
+#ifndef USV_RED_PACKED
+// 1: the LDS transpose stores the 8 packed (cost_x, cost_x+8) words instead of
+// 16 keys (half the ds_write), the reader builds the keys with v_perm from the
+// source lane's disparity (per-lane byte tables); 0: keys stored.
+#define USV_RED_PACKED 1
+#endif
 #ifndef USV_FAST_OCC
 #define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
 #endif
@@ -200,6 +206,37 @@ __device__ __forceinline__ uint32_t reduce16_lds(const uint32_t (&k)[16], uint32
     for (int j = 0; j < 4; ++j) {
         const uint4 q = reinterpret_cast<const uint4*>(tb)[rd[j]];
         v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+    }
+    asm volatile("" ::: "memory");
+    uint32_t a = min(min(v[0], v[1]), v[2]), b = min(min(v[3], v[4]), v[5]);
+    uint32_t c = min(min(v[6], v[7]), v[8]), d = min(min(v[9], v[10]), v[11]);
+    uint32_t e = min(min(v[12], v[13]), v[14]);
+    a = min(min(a, b), c);
+    d = min(min(d, e), v[15]);
+    uint32_t r = min(a, d);
+    r = min(r, dpp<kQuadSwap2>(r));
+    return min(r, dpp<kQuadSwap1>(r));
+}
+
+// Packed variant: lane l stores S[i] (costs of pixels i and i + 8 in the low /
+// high halves) at tb[64 i + l]; lane m = 4p + q reads S[p % 8] of source lanes
+// 16q .. 16q+15 and forms key = (half << 8) | d_src with one v_perm per value:
+// dpk[j] holds the four source disparities of read j as bytes, sel[e] picks
+// byte e of dpk and the low (p < 8) or high (p >= 8) half of the cost.
+__device__ __forceinline__ uint32_t reduce16_lds_packed(const uint32_t (&S)[8], uint32_t* tb, int lane,
+                                                        const uint32_t (&rd)[4], const uint32_t (&dpk)[4],
+                                                        const uint32_t (&sel)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tb[64 * i + lane] = S[i];
+    asm volatile("" ::: "memory");
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 q = reinterpret_cast<const uint4*>(tb)[rd[j]];
+        v[4 * j] = __builtin_amdgcn_perm(q.x, dpk[j], sel[0]);
+        v[4 * j + 1] = __builtin_amdgcn_perm(q.y, dpk[j], sel[1]);
+        v[4 * j + 2] = __builtin_amdgcn_perm(q.z, dpk[j], sel[2]);
+        v[4 * j + 3] = __builtin_amdgcn_perm(q.w, dpk[j], sel[3]);
     }
     asm volatile("" ::: "memory");
     uint32_t a = min(min(v[0], v[1]), v[2]), b = min(min(v[3], v[4]), v[5]);
@@ -377,7 +414,26 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     {
         const int p = lane >> 2, q = lane & 3;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rd[j] = (uint32_t)(16 * p + 4 * q + ((j + p) & 3));
+        for (int j = 0; j < 4; ++j)
+            rd[j] = (uint32_t)(16 * (USV_RED_PACKED ? (p & 7) : p) + 4 * q + ((j + p) & 3));
+    }
+    // packed transpose: source disparities of each read (bytes) and the v_perm selectors
+    uint32_t dpk[4], psel[4];
+    {
+        const int p = lane >> 2, q = lane & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int src = 16 * q + 4 * ((j + p) & 3) + e;
+                w |= (uint32_t)(NW * min(src, lmax) + wave) << (8 * e);
+            }
+            dpk[j] = w;
+        }
+        const uint32_t half = p >= 8 ? 0x00020200u : 0u;  // cost bytes 6,7 (high half) or 4,5 (low)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) psel[e] = (0x0c050400u | half) + (uint32_t)e;
     }
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
@@ -557,13 +613,20 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         cb ^= 1;
     };
     auto emit = [&](const uint32_t(&S)[HALF], int slot) {
+        uint32_t m;
+        if constexpr (USV_RED_PACKED && C::RED_LDS && USV_EXP == 0) {
+            m = reduce16_lds_packed(S, tb, lane, rd, dpk, psel);
+            comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 2)] = m;
+            USV_STAMP(3);
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
         uint32_t keys[K];
 #pragma unroll
         for (int i = 0; i < HALF; ++i) {
             keys[i] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c050400u);         // (S.lo << 8) | d
             keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
         }
-        uint32_t m;
         if constexpr (USV_EXP == 7) {
             m = keys[lane & 15];  // timing only: no cross-lane reduction at all
         } else if constexpr (USV_EXP == 3) {
@@ -779,7 +842,10 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     const int per_cu = resident_blocks_per_cu<RAD, NW>();
     const long slots = (long)cu_count() * per_cu;
     const long NC = (long)P.n_xt * a.batch;
-    long m = slots / NC;
+#ifndef USV_ROUNDS
+#define USV_ROUNDS 1  // workgroup rounds per launch (experiment: >1 = shorter bands, later rounds fill the tail)
+#endif
+    long m = slots * USV_ROUNDS / NC;
     if (m < 1) m = 1;
     if (m > a.H / (2 * WIN)) m = a.H / (2 * WIN) > 0 ? a.H / (2 * WIN) : 1;
     P.m = (int)m;
@@ -788,7 +854,7 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
     // weighted only when every SIMD holds three waves of one round
-    const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
+    const bool three = USV_ROUNDS == 1 && per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
     P.weights = three ? USV_GEN_WEIGHTS : 0x01010101u;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
