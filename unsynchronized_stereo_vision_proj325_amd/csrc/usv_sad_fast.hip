@@ -139,6 +139,20 @@ struct LSeg {
     static_assert(NLD == 5 || NLD == 6 || NLD == 8, "scalar segment is 5, 6 or 8 dwords");
 };
 
+// An L byte that sits at byte 0 of its dword is used as the whole dword: the
+// R operand's bytes 1-3 are zero (LDS-DMA zero-extends), so v_sad_u8 adds
+// L's other three bytes to every lane's sum -- the same amount for every
+// disparity of an output pixel, so the argmin (and the smallest-d tie rule) is
+// unchanged and one SALU per such byte is saved.  The extra cost must not
+// overflow the packed u16 sums: interior tiles only (a window of w consecutive
+// positions holds at most ceil(w/4) such bytes), r <= 5: 11 rows x (11 x 255 +
+// 3 x 765) = 56 100 < 65 536.  Edge tiles replicate byte 0 and keep the mask.
+#ifndef USV_L_WHOLE_WORD
+#define USV_L_WHOLE_WORD 1
+#endif
+template <int RAD, int EDGE>
+constexpr bool kLWholeWord = USV_L_WHOLE_WORD && EDGE == 0 /* kInterior */ && RAD <= 5;
+
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)0, (int)v, CTRL, 0xF, 0xF, false);
@@ -512,6 +526,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             for (int j = 0; j < C::NPOS; ++j) {
                 const int bidx = LS::byte(j);
                 if constexpr (USV_EXP == 4) Lv[j] = lw[(bidx >> 2) & 7];  // timing only: no byte extraction
+                else if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
                 else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
