@@ -105,6 +105,8 @@ struct Cfg {
     static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
     // (r = 6 with two waves sits at the 168-VGPR limit: the DPP rounds need fewer registers)
     static constexpr bool RED_LDS = USV_RED_LDS && !(RAD == 6 && NW == 2);
+    // packed transpose (USV_RED_PACKED): +8 VGPRs of per-lane tables; r = 6 with one wave would spill
+    static constexpr bool RED_PACKED = USV_RED_PACKED && RED_LDS && !(RAD == 6 && NW == 1);
     static constexpr int TB_WORDS = RED_LDS ? K * 64 : 0;
     static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
     static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
@@ -311,6 +313,45 @@ __device__ __forceinline__ void dma_u8_at(const uint8_t* row, uint32_t voff, uin
 }
 
 
+// A whole row's R DMAs under ONE M0 write: the immediate offset of an LDS-DMA
+// moves the LDS destination and the global address alike
+// (scripts/probes/glds_offset_probe.hip), so DMA q uses offset:256 q and a
+// per-lane offset pre-biased by -256 q; the row pointer carries a -kDmaBias
+// bias so that every per-lane offset stays non-negative (the 32-bit VGPR
+// offset is zero-extended).  Saves the M0 write + wait state of every DMA but
+// the first.
+#ifndef USV_DMA_ONE_M0
+#define USV_DMA_ONE_M0 1
+#endif
+constexpr uint32_t kDmaBias = 1024;  // >= 256 (NQ - 1), NQ <= 5
+template <int NQ>
+__device__ __forceinline__ void dma_row(const uint8_t* rr_biased, const uint32_t (&vo)[NQ], uint32_t m0) {
+    static_assert(NQ >= 1 && NQ <= 5, "1..5 DMAs per row");
+    if constexpr (NQ == 1)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %2"
+                     :: "v"(vo[0]), "s"(m0), "s"(rr_biased) : "memory", "m0");
+    else if constexpr (NQ == 2)
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %3\n\t"
+                     "global_load_lds_ubyte %1, %3 offset:256"
+                     :: "v"(vo[0]), "v"(vo[1]), "s"(m0), "s"(rr_biased) : "memory", "m0");
+    else if constexpr (NQ == 3)
+        asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %4\n\t"
+                     "global_load_lds_ubyte %1, %4 offset:256\n\tglobal_load_lds_ubyte %2, %4 offset:512"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(m0), "s"(rr_biased) : "memory", "m0");
+    else if constexpr (NQ == 4)
+        asm volatile("s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %5\n\t"
+                     "global_load_lds_ubyte %1, %5 offset:256\n\tglobal_load_lds_ubyte %2, %5 offset:512\n\t"
+                     "global_load_lds_ubyte %3, %5 offset:768"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(m0), "s"(rr_biased)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %6\n\t"
+                     "global_load_lds_ubyte %1, %6 offset:256\n\tglobal_load_lds_ubyte %2, %6 offset:512\n\t"
+                     "global_load_lds_ubyte %3, %6 offset:768\n\tglobal_load_lds_ubyte %4, %6 offset:1024"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "s"(m0), "s"(rr_biased)
+                     : "memory", "m0");
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
 // vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
 // stores, so lgkmcnt(0) before the barrier is all the hand-off needs.
@@ -429,7 +470,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         const int p = lane >> 2, q = lane & 3;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            rd[j] = (uint32_t)(16 * (USV_RED_PACKED ? (p & 7) : p) + 4 * q + ((j + p) & 3));
+            rd[j] = (uint32_t)(16 * (C::RED_PACKED ? (p & 7) : p) + 4 * q + ((j + p) & 3));
     }
     // packed transpose: source disparities of each read (bytes) and the v_perm selectors
     uint32_t dpk[4], psel[4];
@@ -468,6 +509,9 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     uint32_t colR[C::NQ];
 #pragma unroll
     for (int i = 0; i < C::NQ; ++i) colR[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1);
+    uint32_t colRb[C::NQ];  // dma_row: + kDmaBias - 256 q (the row pointer carries -kDmaBias)
+#pragma unroll
+    for (int i = 0; i < C::NQ; ++i) colRb[i] = colR[i] + kDmaBias - 256u * (uint32_t)i;
     const uint32_t rbase = lds_addr(rbuf);
     // BUF >= 0: compile-time ring slot (static ring); BUF < 0: slot t & (NB-1)
     auto issue_dma = [&](int t, auto buf_tag) {
@@ -477,6 +521,9 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 ((USV_EXP != 1 ? dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase) : void()), ...);
             }(std::make_integer_sequence<int, C::NQ>{});
+        } else if constexpr (USV_DMA_ONE_M0) {
+            const int buf = t & (NB - 1);
+            if (USV_EXP != 1) dma_row<C::NQ>(rr - kDmaBias, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
         } else {
             const int buf = t & (NB - 1);
 #pragma unroll
@@ -629,7 +676,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     };
     auto emit = [&](const uint32_t(&S)[HALF], int slot) {
         uint32_t m;
-        if constexpr (USV_RED_PACKED && C::RED_LDS && USV_EXP == 0) {
+        if constexpr (C::RED_PACKED && USV_EXP == 0) {
             m = reduce16_lds_packed(S, tb, lane, rd, dpk, psel);
             comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 2)] = m;
             USV_STAMP(3);
