@@ -497,10 +497,15 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     const int T = nout + 2 * RAD;  // input rows walked
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
 
-    auto row_ptr = [&](const uint8_t* img, int t) {
+    // Row t's byte offset (clamped row; 32-bit: the host keeps pitch * H < 2^31)
+    // against per-band bases that already carry the constant parts (L's segment
+    // start, R's DMA bias): one multiply and one 64-bit add per pointer per row.
+    auto row_off = [&](int t) -> uint32_t {
         const int y = min(max(y_begin - RAD + t, 0), Hm1);
-        return img + (size_t)y * a.pitch;
+        return (uint32_t)(y * a.pitch);
     };
+    const uint8_t* const Lseg = L + LS::base(x0);
+    const uint8_t* const Rdma = (USV_DMA_ONE_M0 && !C::STATIC_RING) ? R - kDmaBias : R;
 
     // ---- R rows: LDS-DMA into the ring, PD rows ahead ----
     // Rows past the band are clamped to real rows: harmless extra loads.
@@ -516,14 +521,14 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // BUF >= 0: compile-time ring slot (static ring); BUF < 0: slot t & (NB-1)
     auto issue_dma = [&](int t, auto buf_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
-        const uint8_t* rr = row_ptr(R, t);
+        const uint8_t* rr = Rdma + row_off(t);
         if constexpr (BUF >= 0) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 ((USV_EXP != 1 ? dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase) : void()), ...);
             }(std::make_integer_sequence<int, C::NQ>{});
-        } else if constexpr (USV_DMA_ONE_M0) {
+        } else if constexpr (USV_DMA_ONE_M0 && !C::STATIC_RING) {
             const int buf = t & (NB - 1);
-            if (USV_EXP != 1) dma_row<C::NQ>(rr - kDmaBias, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            if (USV_EXP != 1) dma_row<C::NQ>(rr, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
         } else {
             const int buf = t & (NB - 1);
 #pragma unroll
@@ -537,7 +542,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // vector load (the LDS-DMA intrinsic defeats its no-clobber proof) and
     // drain the DMA look-ahead with vmcnt(0).
     LWords lw_next;
-    auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(row_ptr(L, t) + LS::base(x0)); };
+    auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(Lseg + row_off(t)); };
 
 #if USV_STAMPS
     Stamps st;
@@ -952,7 +957,8 @@ extern "C" __attribute__((visibility("default"))) int usv_debug_wgtime(unsigned 
 bool fast_path_supported(const MatchArgs& a) {
     // W % 4 == 0 and W >= 3 tiles: the border tiles' L maps are compile-time
     return a.metric == 0 && a.w >= 3 && a.w <= 15 && (a.w & 1) && a.D >= 1 && a.D <= 256 &&
-           (a.W % 4) == 0 && a.W >= 3 * kK && (a.pitch % 4) == 0 && (reinterpret_cast<uintptr_t>(a.L) % 4) == 0 &&
+           (a.W % 4) == 0 && a.W >= 3 * kK && (a.pitch % 4) == 0 && (long long)a.pitch * a.H < (1LL << 31) &&
+           (reinterpret_cast<uintptr_t>(a.L) % 4) == 0 &&
            (reinterpret_cast<uintptr_t>(a.R) % 4) == 0 && (a.batch <= 1 || a.pair_stride % 4 == 0);
 }
 
