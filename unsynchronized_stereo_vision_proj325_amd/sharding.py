@@ -1,5 +1,9 @@
 """Multi-GPU data parallelism over independent stereo pairs.
 
+Two forms: a batch of pairs, one (or a few) per GPU (weak scaling, configs D / E: pair_range +
+gather_disparity), and one frame split into row bands with halos (strong scaling of config C:
+band_range + match_band + gather_bands).
+
 One process per GPU.  A batch of B frame pairs is partitioned into contiguous
 shards (pair i -> rank i at B = N); every rank block-matches its own pairs with
 no data-path collective, and rank 0 collects the u8 disparity maps with one
@@ -67,3 +71,50 @@ def gather_disparity(local: torch.Tensor, batch: int, dst: int = 0, group=None, 
                 return assemble()
         return _Pending()
     return assemble()
+
+
+# ---- single-frame band sharding (SURVEY.md §8(e), config C at N GPUs) ----
+
+def band_range(H: int, rank: int, world: int, window: int) -> tuple[int, int, int, int]:
+    """Rows of one frame for `rank`: output rows [y0, y1) and the input rows [i0, i1) it reads.
+
+    The input band adds r = (window - 1) / 2 halo rows on each side, cut at the image: the block
+    matcher's row clamp then only ever applies at the true image borders, so a band's output rows
+    are bit-identical to the same rows of the full-frame result (tests/test_sharding.py).
+    """
+    if window < 1 or window % 2 == 0:
+        raise ValueError("window must be odd and positive")
+    y0, y1 = pair_range(H, rank, world)
+    r = (window - 1) // 2
+    return y0, y1, max(0, y0 - r), min(H, y1 + r)
+
+
+def match_band(matcher, left, right, rank: int, world: int, out=None):
+    """Disparity of rank's output rows of one (H, W) frame: the matcher runs on the halo'd input
+    band (a row view, no copy) and the band's own rows are returned (a view of `out` if given)."""
+    H = left.shape[0]
+    y0, y1, i0, i1 = band_range(H, rank, world, matcher.window)
+    full = matcher.compute(left[i0:i1], right[i0:i1], out_disp=out)
+    return full[y0 - i0:y1 - i0]
+
+
+def gather_bands(local, H: int, dst: int = 0, group=None, recv: list | None = None):
+    """Collect every rank's (y1 - y0, W) u8 band into the (H, W) frame on `dst` (one gather; ranks
+    pad to the largest band).  Returns the frame on dst, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    y0, y1 = pair_range(H, rank, world)
+    if local.shape[0] != y1 - y0:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, band is {y1 - y0}")
+    width = max(pair_range(H, r, world)[1] - pair_range(H, r, world)[0] for r in range(world))
+    send = local
+    if local.shape[0] < width:
+        send = torch.cat([local, torch.zeros((width - local.shape[0],) + tuple(local.shape[1:]),
+                                             dtype=local.dtype, device=local.device)], 0)
+    bufs = None
+    if rank == dst:
+        bufs = recv if recv is not None else [torch.empty_like(send) for _ in range(world)]
+    dist.gather(send.contiguous(), bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([bufs[r][:pair_range(H, r, world)[1] - pair_range(H, r, world)[0]] for r in range(world)], 0)
