@@ -26,7 +26,21 @@ void IDMatcher(std::vector<Match> InterframeMatchIndexes,
                std::vector<Match> OldInterframeMatchIndexes,
                std::vector<cv::Point3i>& InterframeMatchIndexesComplete);
 
+// P/Main.cpp:1120-1143 (Canny copy P/Main.cpp:628-654): for each tentative
+// match, the centre of minAreaRect(Contours[LeftIndex]) -- the four
+// RotatedRect corners summed as Point2f and divided by 4 -- appended to
+// VectorCenter_point.  Not a function in the reference (inline in its thread
+// body); named here so a caller can reach it.
+void MatchCentroids(const std::vector<std::vector<cv::Point> >& Contours,
+                    const std::vector<Match>& TentativeMatch,
+                    std::vector<cv::Point2f>& VectorCenter_point);
+
 namespace usv {
+// OpenCV 3.0 convexHull(pts, hull, clockwise=true) and minAreaRect (Sklansky +
+// rotating calipers), restated; parity unpinned.
+std::vector<cv::Point> convexHullCW(const std::vector<cv::Point>& pts);
+cv::RotatedRect minAreaRect(const std::vector<cv::Point>& points);
+cv::Point2f rectCentre(const cv::RotatedRect& r);
 // OpenCV 3.0 matchShapes(c1, c2, CONTOURS_MATCH_I1, 0) and contourArea(c, false),
 // restated (OpenCV is not in the image; parity unpinned).
 double matchShapesI1(const std::vector<cv::Point>& a, const std::vector<cv::Point>& b);

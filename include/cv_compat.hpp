@@ -12,7 +12,9 @@
 //     (Point2f / float stays a float operation);
 //   * Vec<T, n>(T v0) is non-explicit and zero-fills the tail, and
 //     Point3_(const Vec<T,3>&) is non-explicit, so (Point3i)(unsigned u) is
-//     (u, 0, 0) -- the conversion P/Main.cpp:492 relies on.
+//     (u, 0, 0) -- the conversion P/Main.cpp:492 relies on;
+//   * RotatedRect {center, size, angle(deg)} and points() in OpenCV's corner order
+//     (the centroid step, P/Main.cpp:1129-1139).
 #pragma once
 
 #if defined(__has_include)
@@ -24,6 +26,7 @@
 #ifdef USV_HAVE_OPENCV
 #include <opencv2/opencv.hpp>
 #else
+#include <cmath>
 #include <cstddef>
 
 namespace cv {
@@ -113,6 +116,40 @@ USV_CV_SCALAR_OPS(int)
 USV_CV_SCALAR_OPS(float)
 USV_CV_SCALAR_OPS(double)
 #undef USV_CV_SCALAR_OPS
+
+
+template <typename T>
+class Size_ {
+public:
+    T width, height;
+    Size_() : width(0), height(0) {}
+    Size_(T w, T h) : width(w), height(h) {}
+};
+typedef Size_<float> Size2f;
+
+// OpenCV 3.0 RotatedRect: centre, (width, height), angle in degrees.
+class RotatedRect {
+public:
+    Point2f center;
+    Size2f size;
+    float angle;
+    RotatedRect() : center(), size(), angle(0) {}
+    RotatedRect(const Point2f& c, const Size2f& s, float a) : center(c), size(s), angle(a) {}
+    // The four corners, OpenCV's order and float arithmetic (double angle -> float cos/sin * 0.5f).
+    void points(Point2f pt[]) const {
+        const double a_rad = angle * 3.14159265358979323846 / 180.;
+        const float b = (float)std::cos(a_rad) * 0.5f;
+        const float a = (float)std::sin(a_rad) * 0.5f;
+        pt[0].x = center.x - a * size.height - b * size.width;
+        pt[0].y = center.y + b * size.height - a * size.width;
+        pt[1].x = center.x + a * size.height - b * size.width;
+        pt[1].y = center.y - b * size.height - a * size.width;
+        pt[2].x = 2 * center.x - pt[0].x;
+        pt[2].y = 2 * center.y - pt[0].y;
+        pt[3].x = 2 * center.x - pt[1].x;
+        pt[3].y = 2 * center.y - pt[1].y;
+    }
+};
 
 }  // namespace cv
 #endif  // USV_HAVE_OPENCV

@@ -29,6 +29,8 @@
  *   usv_generate_matching_list GenerateMatchingList, P/Main.cpp:403-426
  *                             (OpenCV matchShapes/contourArea restated; parity
  *                             unpinned -- OpenCV 3.0 is absent).
+ *   usv_min_area_rect,        minAreaRect + the per-match centre point,
+ *   usv_match_centroids       P/Main.cpp:1120-1143 (A7; OpenCV restated, unpinned).
  *   usv_rectify_params / _map initUndistortRectifyMap(..., CV_16SC2, ...),
  *                             P/Main.cpp:352,357 (the
  *                             reference rebuilds it every frame, we build once)
@@ -155,6 +157,21 @@ usv_status usv_generate_matching_list(const int* pts_a, const int* off_a, int n_
 /* Hu-moment I1 distance (OpenCV CONTOURS_MATCH_I1) and unoriented polygon area. */
 double usv_match_shapes_i1(const int* pts_a, int n_a, const int* pts_b, int n_b);
 double usv_contour_area(const int* pts, int n);
+
+/*
+ * minAreaRect (OpenCV 3.0 restated) of n int (x,y) points: out5 = {centre.x,
+ * centre.y, width, height, angle in degrees}.  P/Main.cpp:1129.
+ */
+usv_status usv_min_area_rect(const int* pts, int n, float* out5);
+
+/*
+ * The centroid step of P/Main.cpp:1120-1143: for each match (in order) whose
+ * left_index names one of the n_contours contours (flattened as for
+ * usv_generate_matching_list), the centre of that contour's minAreaRect as
+ * float (x, y) into out_xy (2*n_matches floats); *n_out gets the count.
+ */
+usv_status usv_match_centroids(const int* pts, const int* off, int n_contours, const usv_match* matches,
+                               int n_matches, float* out_xy, int* n_out);
 
 /*
  * MovingObjectDistanceCalculator over arrays (see oracle/usv_oracle.h for the

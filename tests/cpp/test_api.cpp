@@ -84,5 +84,16 @@ int main() {
     print_matches("generate", M);
     ResolveMatchList(M, TentativeMatch);
     print_matches("generate_resolved", TentativeMatch);
+
+    // ---- centre points of the matched contours (P/Main.cpp:1120-1143 pattern) ----
+    std::vector<Point2f> VectorCenter_point;
+    MatchCentroids(A, TentativeMatch, VectorCenter_point);
+    printf("{\"centroids\": [");
+    for (size_t i = 0; i < VectorCenter_point.size(); ++i) {
+        pnum(i ? ", [" : "[", VectorCenter_point[i].x);
+        pnum(", ", VectorCenter_point[i].y);
+        printf("]");
+    }
+    printf("]}\n");
     return 0;
 }

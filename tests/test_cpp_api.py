@@ -50,3 +50,11 @@ def test_generate(cpp_out):
     B = [[(5, 5), (45, 5), (45, 15), (5, 15)], [(1, 1), (21, 1), (21, 21), (1, 21)]]
     assert cpp_out["generate"] == [list(t) for t in host.GenerateMatchingList(A, B)]
     assert cpp_out["generate_resolved"] == [list(t) for t in host.ResolveMatchList(host.GenerateMatchingList(A, B))]
+
+
+def test_centroids(cpp_out):
+    A = [[(0, 0), (20, 0), (20, 20), (0, 20)], [(0, 0), (40, 0), (40, 10), (0, 10)]]
+    B = [[(5, 5), (45, 5), (45, 15), (5, 15)], [(1, 1), (21, 1), (21, 21), (1, 21)]]
+    t = host.ResolveMatchList(host.GenerateMatchingList(A, B))
+    assert cpp_out["centroids"] == [list(c) for c in host.MatchCentroids(A, t)]
+    assert len(cpp_out["centroids"]) == len(t) > 0

@@ -67,6 +67,9 @@ SIGNATURES = {
                                            POINTER(c_int)]),
     "usv_match_shapes_i1": (c_double, [POINTER(c_int), c_int, POINTER(c_int), c_int]),
     "usv_contour_area": (c_double, [POINTER(c_int), c_int]),
+    "usv_min_area_rect": (c_int, [POINTER(c_int), c_int, POINTER(c_float)]),
+    "usv_match_centroids": (c_int, [POINTER(c_int), POINTER(c_int), c_int, POINTER(usv_match), c_int,
+                                    POINTER(c_float), POINTER(c_int)]),
     "usv_moving_object_distance": (c_int, [c_int, c_int64, POINTER(c_float), c_int, POINTER(c_float),
                                            c_int, POINTER(c_float), c_int, POINTER(c_float), c_int,
                                            POINTER(c_int), c_int, c_int64, c_int64, c_int64,

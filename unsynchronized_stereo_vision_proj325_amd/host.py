@@ -6,6 +6,7 @@ include/DistanceCalculator.hpp.  Function names follow the reference:
   ResolveMatchList            P/Main.cpp:432-477
   IDMatcher                   P/Main.cpp:483-499
   GenerateMatchingList        P/Main.cpp:403-426 (OpenCV maths restated; parity unpinned)
+  MatchCentroids              P/Main.cpp:1120-1143 (minAreaRect restated; parity unpinned)
   MovingObjectDistanceCalculator  P/DistanceCalculator.cpp:15-88
   CooridinatePositionCalculator   P/DistanceCalculator.cpp:90-141 (reference spelling)
 """
@@ -83,6 +84,29 @@ def contour_area(c) -> float:
     lib = _lib.load()
     p = np.ascontiguousarray(np.asarray(c, dtype=np.int32).reshape(-1))
     return lib.usv_contour_area(p.ctypes.data_as(POINTER(c_int)), len(c))
+
+
+def min_area_rect(c):
+    """OpenCV 3.0 minAreaRect of int points -> ((cx, cy), (w, h), angle_deg), float32 values."""
+    lib = _lib.load()
+    p = np.ascontiguousarray(np.asarray(c, dtype=np.int32).reshape(-1)) if len(c) else np.zeros(2, np.int32)
+    out = (c_float * 5)()
+    _lib.check("usv_min_area_rect", lib.usv_min_area_rect(p.ctypes.data_as(POINTER(c_int)), len(c), out))
+    return (out[0], out[1]), (out[2], out[3]), out[4]
+
+
+def MatchCentroids(contours, tentative_match):
+    """Centre point of minAreaRect(contours[left]) per match (P/Main.cpp:1120-1143) -> list[(x, y)] float32."""
+    lib = _lib.load()
+    p, off = _flatten(contours)
+    m = _matches(tentative_match)
+    out = (c_float * max(2 * len(tentative_match), 2))()
+    n = c_int(0)
+    ip = POINTER(c_int)
+    _lib.check("usv_match_centroids", lib.usv_match_centroids(
+        p.ctypes.data_as(ip), off.ctypes.data_as(ip), len(contours), m, len(tentative_match), out,
+        ctypes.byref(n)))
+    return [(out[2 * i], out[2 * i + 1]) for i in range(n.value)]
 
 
 def _f32(pts):
