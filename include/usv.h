@@ -31,6 +31,8 @@
  *                             unpinned -- OpenCV 3.0 is absent).
  *   usv_min_area_rect,        minAreaRect + the per-match centre point,
  *   usv_match_centroids       P/Main.cpp:1120-1143 (A7; OpenCV restated, unpinned).
+ *   usv_contour_descriptors,  GPU form of GenerateMatchingList's scores
+ *   usv_contour_pair_scores   (SURVEY §8(f) row 2), descriptors once per contour.
  *   usv_rectify_params / _map initUndistortRectifyMap(..., CV_16SC2, ...),
  *                             P/Main.cpp:352,357 (the
  *                             reference rebuilds it every frame, we build once)
@@ -172,6 +174,19 @@ usv_status usv_min_area_rect(const int* pts, int n, float* out5);
  */
 usv_status usv_match_centroids(const int* pts, const int* off, int n_contours, const usv_match* matches,
                                int n_matches, float* out_xy, int* n_out);
+
+/*
+ * GPU contour matcher (GenerateMatchingList's scores,
+ * P/Main.cpp:408-424).  Device pointers, flattened as for
+ * usv_generate_matching_list.  usv_contour_descriptors writes n x 8 doubles per
+ * contour set: the 7 I1 terms 1/(sign(h) log10|h|) of its Hu invariants (NaN
+ * where |h| <= 1e-5) and its unoriented area.  usv_contour_pair_scores writes
+ * the n_a x n_b score matrix (i-major) = I1 + |(A_i - A_j)/((A_i + A_j)/2)|;
+ * the caller keeps scores < 0.75 in i-major order.
+ */
+usv_status usv_contour_descriptors(const int* pts, const int* off, int n, double* desc, void* stream);
+usv_status usv_contour_pair_scores(const double* desc_a, int n_a, const double* desc_b, int n_b, double* scores,
+                                   void* stream);
 
 /*
  * MovingObjectDistanceCalculator over arrays (see oracle/usv_oracle.h for the

@@ -1,0 +1,77 @@
+"""GPU contour matcher vs the host GenerateMatchingList restatement.
+
+The device descriptors follow csrc/host/matching.cpp's f64 operation order, so
+areas are bit-identical and Hu-based I1 scores agree to a few ulp (log10 is the
+only libm function; device and host libm may round it differently): the test
+tolerance is 1e-12 relative.  Parity with OpenCV itself is unpinned (OpenCV 3.0
+is absent; tests/test_matching.py).
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from unsynchronized_stereo_vision_proj325_amd import host
+from unsynchronized_stereo_vision_proj325_amd.contours import (GenerateMatchingListGPU, contour_descriptors,
+                                                               contour_pair_scores)
+
+pytestmark = pytest.mark.gpu
+
+
+def _blob(rng, n):
+    cx, cy, r = rng.randint(20, 600), rng.randint(20, 440), rng.randint(4, 60)
+    ang = sorted(rng.uniform(0, 2 * math.pi) for _ in range(n))
+    return [(int(cx + r * rng.uniform(0.5, 1.0) * math.cos(a)), int(cy + r * rng.uniform(0.5, 1.0) * math.sin(a)))
+            for a in ang]
+
+
+def _sets(seed, n_a, n_b):
+    rng = random.Random(seed)
+    A = [_blob(rng, rng.randint(3, 120)) for _ in range(n_a)]
+    B = [_blob(rng, rng.randint(3, 120)) for _ in range(n_b)]
+    B[:3] = [[(x + 31, y - 7) for x, y in c] for c in A[:3]]  # translated copies: score ~0
+    A.append([(0, 0), (5, 0), (10, 0)])  # zero area
+    B.append([(2, 2)])
+    return A, B
+
+
+@pytest.mark.parametrize("seed,n_a,n_b", [(0, 5, 7), (1, 40, 33), (2, 150, 170)])
+def test_scores_match_host(seed, n_a, n_b):
+    A, B = _sets(seed, n_a, n_b)
+    s = contour_pair_scores(contour_descriptors(A), contour_descriptors(B)).cpu().numpy()
+    for i, a in enumerate(A):
+        for j, b in enumerate(B):
+            ref = host.match_shapes_i1(a, b)
+            aa, ab = host.contour_area(a), host.contour_area(b)
+            ref += abs((aa - ab) / ((aa + ab) / 2)) if (aa + ab) != 0 else float("nan")
+            got = s[i, j]
+            if math.isnan(ref) or math.isinf(ref):
+                assert (math.isnan(got) and math.isnan(ref)) or got == ref, (i, j, got, ref)
+            else:
+                assert math.isclose(got, ref, rel_tol=1e-12, abs_tol=1e-15), (i, j, got, ref)
+
+
+def test_areas_bit_identical():
+    A, _ = _sets(3, 60, 1)
+    d = contour_descriptors(A).cpu().numpy()
+    assert [float(v) for v in d[:, 7]] == [host.contour_area(c) for c in A]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_generate_matching_list_gpu_equals_host(seed):
+    A, B = _sets(10 + seed, 25, 30)
+    got, ref = GenerateMatchingListGPU(A, B), host.GenerateMatchingList(A, B)
+    assert [(i, j) for i, j, _ in got] == [(i, j) for i, j, _ in ref]
+    assert np.allclose([v for *_, v in got], [v for *_, v in ref], rtol=1e-12, atol=1e-15)
+    assert all((k, k) in {(i, j) for i, j, _ in got} for k in range(3))
+
+
+def test_empty_sets():
+    A, B = _sets(5, 3, 3)
+    assert GenerateMatchingListGPU([], B) == [] and GenerateMatchingListGPU(A, []) == []
+    assert contour_descriptors([]).shape == (0, 8)
+    s = contour_pair_scores(contour_descriptors(A), contour_descriptors([]))
+    assert s.shape == (len(A), 0)
+    torch.cuda.synchronize()
