@@ -68,6 +68,12 @@ def parse():
     return p.parse_args()
 
 
+def _config_name(W, H, w, D) -> str:
+    """BASELINE.json config letter for these dimensions (A..E), else "custom"."""
+    return {(320, 240, 5, 32): "A", (640, 480, 7, 64): "B", (1920, 1080, 11, 128): "C",
+            (3840, 2160, 15, 256): "E"}.get((W, H, w, D), "custom")
+
+
 def profile_counters(workload_key: str):
     """Per-launch counters of the committed rocprofv3 run for this workload
     (profiles/counters.json, written by scripts/summarize_profile.py), or None."""
@@ -310,7 +316,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded uniform u8 L, slab-shifted R with +-2 noise; SURVEY.md 8(d))",
         "config": {
-            "workload": f"C: {W}x{H} u8 rectified pair, {w}x{w} SAD, D={D}, argmin u8 disparity"
+            "workload": f"{_config_name(W, H, w, D)}: {W}x{H} u8 rectified pair, {w}x{w} SAD, D={D}, argmin u8 disparity"
                         + (" + fused f64 distance map (P/DistanceCalculator.cpp:84)" if with_dist else ""),
             "pairs_per_step": 1 if bands else world,
             "parallelism": (f"one frame in {world} row bands with {w // 2}-row halos, rank-0 RCCL gather of u8 "

@@ -776,6 +776,7 @@ struct BandPlan {
     int m;         // bands per column (pair, x-tile)
     int gen_g;     // workgroups per dispatch generation per XCD (4 SIMDs x CUs per XCD / waves per WG)
     unsigned weights;  // byte g: relative band height of generation g (g >= 3 use byte 3)
+    int extra;     // single pair only: x-tiles 0..extra-1 carry m + 1 bands (fills every resident slot)
 };
 
 // r = 7 (15-row ring) and r = 6 with four waves need more than 168 VGPRs:
@@ -811,7 +812,12 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
     const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
     const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
     const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
-    const unsigned col_xt = tile % nxt, s = (tile / nxt) % (unsigned)P.m, pair = tile / per_pair;
+    // tiles past nxt * m (P.extra > 0, one pair) are band m of x-tiles 0..extra-1
+    const bool past = tile >= per_pair && P.extra > 0;
+    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
+    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
+    const unsigned pair = past ? 0u : tile / per_pair;
+    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
     const unsigned long_run = base + 1u, split = rem * long_run;
     auto gen_weight = [&](unsigned sb) -> unsigned {
         const unsigned t = pair * per_pair + sb * nxt + col_xt;  // tile carrying band sb of this column
@@ -820,7 +826,7 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
         return (P.weights >> (8 * g)) & 0xFFu;
     };
     unsigned pre = 0, tot = 0;
-    for (unsigned sb = 0; sb < (unsigned)P.m; ++sb) {
+    for (unsigned sb = 0; sb < m_col; ++sb) {
         const unsigned wgt = gen_weight(sb);
         pre += sb < s ? wgt : 0u;
         tot += wgt;
@@ -894,9 +900,12 @@ int cu_count() {
 
 // Relative band heights by dispatch generation, three resident waves per SIMD
 // (config C, profiles/probes/wgtime_*.txt: equal bands took 61.5 / 70.0 /
-// 84.0 us by generation; one refinement step of heights ~ 1/time).
+// 84.0 us by generation; one refinement step of heights ~ 1/time gave
+// 100 : 85 : 63).  Since every SIMD holds three waves (P.extra), flatter
+// heights won: interleaved A/B 100:80:58 / 85:63 / 90:70 / 94:78 / 97:85 =
+// 80.5 / 79.1 / 76.8 / 77.9 / 78.7 us (profiles/probes/ab_extra_weights_r01.txt).
 #ifndef USV_GEN_WEIGHTS
-#define USV_GEN_WEIGHTS 0x3F3F5564u  // 100, 85, 63, 63
+#define USV_GEN_WEIGHTS 0x46465A64u  // 100, 90, 70, 70
 #endif
 
 template <int RAD, int NW>
@@ -916,7 +925,14 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     if (m < 1) m = 1;
     if (m > a.H / (2 * WIN)) m = a.H / (2 * WIN) > 0 ? a.H / (2 * WIN) : 1;
     P.m = (int)m;
-    const long total = NC * m;
+#ifndef USV_EXTRA_BANDS
+#define USV_EXTRA_BANDS 1  // one pair: give some x-tiles an extra band so the grid fills every resident slot
+#endif
+    // e.g. 1080p, D = 128: 1536 slots over 120 x-tiles = 12 bands + 96 x-tiles with a 13th
+    const long ex = slots * USV_ROUNDS - NC * m;
+    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && USV_ROUNDS == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= 2 * WIN) ? (int)ex : 0;
+    const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
