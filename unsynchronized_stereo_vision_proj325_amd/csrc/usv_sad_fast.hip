@@ -921,9 +921,17 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 #ifndef USV_ROUNDS
 #define USV_ROUNDS 1  // workgroup rounds per launch (experiment: >1 = shorter bands, later rounds fill the tail)
 #endif
+#ifndef USV_MIN_BAND_WINS
+// shortest band, in windows (w rows): the ring warm-up costs w rows per band.  Binds only on small frames
+// (1080p, D = 128 has 12-13 bands of ~85 rows); interleaved A/B at 640x480 w7 D64: 1 / 2 / 3 / 4 windows =
+// 29.5 / 22.2 / 20.5 / 22.5 us, at 320x240 w5 D32: 2 / 3 / 4 = 16.8 / 15.3 / 16.4 us
+// (profiles/probes/ab_minband_small_r01.txt, ab_weights_minband_r01.txt).
+#define USV_MIN_BAND_WINS 3
+#endif
     long m = slots * USV_ROUNDS / NC;
     if (m < 1) m = 1;
-    if (m > a.H / (2 * WIN)) m = a.H / (2 * WIN) > 0 ? a.H / (2 * WIN) : 1;
+    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    if (m > m_max) m = m_max;
     P.m = (int)m;
 #ifndef USV_EXTRA_BANDS
 #define USV_EXTRA_BANDS 1  // one pair: give some x-tiles an extra band so the grid fills every resident slot
@@ -931,7 +939,7 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     // e.g. 1080p, D = 128: 1536 slots over 120 x-tiles = 12 bands + 96 x-tiles with a 13th
     const long ex = slots * USV_ROUNDS - NC * m;
     P.extra = (USV_EXTRA_BANDS && a.batch == 1 && USV_ROUNDS == 1 && ex > 0 && ex < P.n_xt &&
-               a.H / (m + 1) >= 2 * WIN) ? (int)ex : 0;
+               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
