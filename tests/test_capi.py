@@ -30,7 +30,7 @@ def test_cpp_api_symbols_exported():
     out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
     for mangled in ["_ZN5MatchC1Ejjd", "ResolveMatchList", "IDMatcher", "GenerateMatchingList",
                     "MovingObjectDistanceCalculator", "CooridinatePositionCalculator", "CoordinateDisplay",
-                    "_Z7deg2radd", "_Z7rad2degd"]:
+                    "_Z7deg2radd", "_Z7rad2degd", "MatchCentroids", "minAreaRect"]:
         assert mangled in out, mangled
 
 
@@ -52,6 +52,13 @@ def test_argument_validation_needs_no_gpu(usvlib):
     assert usvlib.usv_sad_disparity_ex(p, p, 64, 64, 64, 16, 5, 1, p, 64, None, 0, None, 1, None) == \
         _lib.USV_ERR_UNSUPPORTED  # SSD forced onto the fast kernel
     assert usvlib.usv_disparity_to_distance(p, 0, 4, 4, p, p, 4, None) == _lib.USV_ERR_INVALID_ARG
+    # GPU contour matcher: bad sizes / null outputs rejected, empty sets are a no-op (no launch)
+    assert usvlib.usv_contour_descriptors(p, p, -1, p, None) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_contour_descriptors(p, None, 3, p, None) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_contour_descriptors(None, None, 0, None, None) == _lib.USV_OK
+    assert usvlib.usv_contour_pair_scores(p, 3, None, 2, p, None) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_contour_pair_scores(p, 3, p, 0, None, None) == _lib.USV_OK
+    assert usvlib.usv_contour_pair_scores(p, 1 << 16, p, 1 << 16, p, None) == _lib.USV_ERR_UNSUPPORTED
 
 
 @pytest.mark.parametrize("model", ["moving_object", "canny"])
