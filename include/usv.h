@@ -3,9 +3,11 @@
  *
  * Plain pointers and sizes only (no HIP, torch or OpenCV types), so any FFI can
  * bind it (see INTEGRATION.md for the ctypes stub and the C++ call sites).
- * Every entry point is thread-safe and reentrant: no global mutable state;
- * work is enqueued on the caller's HIP stream (passed as an opaque void*,
- * NULL = the default stream) and never synchronises the device.
+ * Every entry point is thread-safe and reentrant; the only global state is a
+ * mutex-guarded, append-only cache of device copies of host distance tables
+ * (see usv_sad_disparity_ex).  Work is enqueued on the caller's HIP stream
+ * (passed as an opaque void*, NULL = the default stream) and never
+ * synchronises the device, except that cache's one-time fill.
  *
  * Drop-in map (reference = 6dwavenminer/Unsynchronized_Stereo_Vision_Proj325,
  * P/ = Unsynchronized_Stereo_Vision_Proj325/):
@@ -103,8 +105,12 @@ usv_status usv_sad_disparity(const uint8_t* L, const uint8_t* R, int W, int H, i
 
 /*
  * As usv_sad_disparity, plus (when dist_cm != NULL) the fused per-pixel
- * distance map dist_cm[y*dist_pitch + x] = lut_cm[disp[y][x]] (doubles;
- * lut_cm = DEVICE pointer to 256 doubles from usv_distance_lut_cm).
+ * distance map dist_cm[y*dist_pitch + x] = lut_cm[disp[y][x]] (doubles).
+ * lut_cm = 256 doubles from usv_distance_lut_cm, in device memory, pinned host
+ * memory, or ordinary HOST memory: a pageable host table is copied to a
+ * library-owned device buffer on its first use (one synchronous 2 KB copy per
+ * device and distinct contents, at most 64 tables; make that first call before
+ * any hipGraph capture) and found again by value afterwards.
  * kernel selects the implementation (USV_KERNEL_AUTO normally).
  */
 usv_status usv_sad_disparity_ex(const uint8_t* L, const uint8_t* R, int W, int H, int pitch,
@@ -126,7 +132,8 @@ usv_status usv_sad_disparity_batch(const uint8_t* L, const uint8_t* R, int batch
 /* HOST: lut_out[d] = distance(d) in cm for d = 0..255 (d = 0 -> +inf for model 0). */
 usv_status usv_distance_lut_cm(int model, double* lut_out);
 
-/* DEVICE: out[y*out_pitch + x] = lut_cm[disp[y*disp_pitch + x]] (doubles). */
+/* DEVICE: out[y*out_pitch + x] = lut_cm[disp[y*disp_pitch + x]] (doubles);
+ * lut_cm in device or host memory, as for usv_sad_disparity_ex. */
 usv_status usv_disparity_to_distance(const uint8_t* disp, int W, int H, int disp_pitch,
                                      const double* lut_cm, double* out, int out_pitch,
                                      void* stream);
@@ -189,16 +196,24 @@ usv_status usv_contour_pair_scores(const double* desc_a, int n_a, const double* 
                                    void* stream);
 
 /*
- * MovingObjectDistanceCalculator over arrays (see oracle/usv_oracle.h for the
- * argument meaning).  Appends up to n_triples doubles to dist_out; *n_out gets
- * the count; interp_out (nullable, 2*n_triples floats) receives the
- * extrapolated other-camera centroids.
+ * MovingObjectDistanceCalculator over arrays, arguments in the reference's
+ * order (P/DistanceCalculator.hpp:37-46).  Points are interleaved float (x, y),
+ * triples int (x, y, z), time stamps steady_clock ticks (ns).
+ *   interp_in / n_interp_in : the caller's InterpolatedVectorCenter_pointOtherCamera
+ *                (by value in the reference; P/Main.cpp passes it empty).  The
+ *                reference pushes one extrapolated point per triple onto its copy
+ *                and reads element i of the grown vector (P/DistanceCalculator.cpp:67,75-80),
+ *                so a non-empty vector shifts which point triple i is measured against.
+ * Appends up to n_triples doubles to dist_out; *n_out gets the count;
+ * interp_out (nullable, 2*(n_interp_in + n_triples) floats) receives the grown
+ * vector: the caller's points, then the extrapolated other-camera centroids.
  */
 usv_status usv_moving_object_distance(int camera_side_left, int64_t ts_this,
                                       const float* this_pts, int n_this,
                                       const float* cur_pts, int n_cur,
                                       const float* old_pts, int n_old,
                                       const float* older_pts, int n_older,
+                                      const float* interp_in, int n_interp_in,
                                       const int* triples, int n_triples,
                                       int64_t ts_other, int64_t ts_other_old,
                                       int64_t ts_other_older,

@@ -10,6 +10,7 @@
 #include "usv_oracle.h"
 #include <math.h>
 #include <stddef.h>
+#include <stdlib.h>
 
 #define USV_PI 3.14159265 /* P/DistanceCalculator.hpp:25 -- NOT M_PI */
 #define USV_CAMERA_DIST_CM 20.16
@@ -59,6 +60,14 @@ int usv_oracle_moving_object_distance(int camera_side_left, int64_t ts_this,
                                       double* dist_out) {
     /* P/DistanceCalculator.cpp:28 -- all three other-camera vectors non-empty */
     if (n_cur <= 0 || n_old <= 0 || n_older <= 0) return 0;
+    if (n_interp_in < 0) n_interp_in = 0;
+    /* The by-value InterpolatedVectorCenter_pointOtherCamera copy (line 19):
+     * the caller's n_interp_in points, then one point pushed per triple
+     * (line 67).  Line 75 reads element i of it. */
+    float* grown = (float*)malloc(sizeof(float) * 2 * ((size_t)n_interp_in + (size_t)(n_triples > 0 ? n_triples : 0) + 1));
+    if (!grown) return -1;
+    for (int k = 0; k < 2 * n_interp_in; ++k) grown[k] = interp_in[k];
+    int n_grown = n_interp_in;
     int appended = 0;
     for (int i = 0; i < n_triples; ++i) {
         int tx = triples[3 * i + 0], ty = triples[3 * i + 1], tz = triples[3 * i + 2];
@@ -77,11 +86,13 @@ int usv_oracle_moving_object_distance(int camera_side_left, int64_t ts_this,
         float v3x = v2x + (ax * t3), v3y = v2y + (ay * t3);
         float px = (v3x * t3) + cx, py = (v3y * t3) + cy;
         /* line 67 pushes onto the by-value copy; line 75 then reads index i of
-         * that copy, which is the caller's element i when the caller passed a
-         * non-empty vector (a reference quirk kept here). */
-        float ix, iy;
-        if (i < n_interp_in) { ix = interp_in[2 * i]; iy = interp_in[2 * i + 1]; }
-        else { ix = px; iy = py; }
+         * that copy: the caller's element i while i < n_interp_in, else the
+         * point pushed at iteration i - n_interp_in (a reference quirk kept
+         * here; with an empty caller vector that is this iteration's point). */
+        grown[2 * n_grown] = px;
+        grown[2 * n_grown + 1] = py;
+        ++n_grown;
+        float ix = grown[2 * i], iy = grown[2 * i + 1];
         /* lines 69-83 -- interp index i is always in range after the push */
         int dispx = 0, dispy = 0, disp = 0;
         if (n_this > 0 && n_this > i) {
@@ -92,6 +103,7 @@ int usv_oracle_moving_object_distance(int camera_side_left, int64_t ts_this,
         }
         dist_out[appended++] = usv_oracle_distance_cm(disp);
     }
+    free(grown);
     return appended;
 }
 

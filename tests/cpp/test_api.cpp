@@ -59,6 +59,20 @@ int main() {
     for (size_t i = 0; i < dist.size(); ++i) pnum(i ? ", " : "", dist[i]);
     printf("]}\n");
 
+    // a non-empty caller vector, shorter (1 < 3 triples) and longer (5 > 3) than the triple list
+    // (P/DistanceCalculator.cpp:67,75-80 read element i of the grown by-value copy)
+    const std::vector<std::vector<Point2f> > interps = {
+        {Point2f(250.f, 190.f)},
+        {Point2f(250.f, 190.f), Point2f(60.f, 40.f), Point2f(1.f, 2.f), Point2f(3.f, 4.f), Point2f(5.f, 6.f)}};
+    for (size_t k = 0; k < interps.size(); ++k) {
+        std::vector<double> d2;
+        MovingObjectDistanceCalculator(LeftCam, at(1040000000LL), thisPts, curO, oldO, olderO, interps[k], tri,
+                                       at(1033000000LL), at(1000000000LL), at(966000000LL), d2);
+        printf("{\"dist_interp%zu\": [", k);
+        for (size_t i = 0; i < d2.size(); ++i) pnum(i ? ", " : "", d2[i]);
+        printf("]}\n");
+    }
+
     vector<Point3d> pos;
     CooridinatePositionCalculator(LeftCam, dist, thisPts, pos);  // CoordinateDisplay false: nothing
     printf("{\"pos_off\": %zu}\n", pos.size());

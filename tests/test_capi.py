@@ -98,16 +98,18 @@ def test_resolve_and_idmatcher_vs_oracle(oracle):
         assert got == [tuple(xyz[3 * i:3 * i + 3]) for i in range(k)]
 
 
-def _oracle_mo(oracle, side, ts, this, cur, old, older, tri, t0, t1, t2):
+def _oracle_mo(oracle, side, ts, this, cur, old, older, tri, t0, t1, t2, interp=()):
     f = lambda a: (np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1)))  # noqa: E731
-    a, b, c, d = f(this), f(cur), f(old), f(older)
+    a, b, c, d, e = f(this), f(cur), f(old), f(older), f(interp)
     tr = np.ascontiguousarray(np.asarray(tri, dtype=np.int32).reshape(-1))
     out = np.zeros(max(len(tr) // 3, 1), dtype=np.float64)
     FP, IP, DP = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)
     n = oracle.usv_oracle_moving_object_distance(
         int(side), ts, a.ctypes.data_as(FP), len(a) // 2, b.ctypes.data_as(FP), len(b) // 2,
-        c.ctypes.data_as(FP), len(c) // 2, d.ctypes.data_as(FP), len(d) // 2, None, 0,
+        c.ctypes.data_as(FP), len(c) // 2, d.ctypes.data_as(FP), len(d) // 2,
+        e.ctypes.data_as(FP) if len(e) else None, len(e) // 2,
         tr.ctypes.data_as(IP), len(tr) // 3, t0, t1, t2, out.ctypes.data_as(DP))
+    assert n >= 0
     return out[:n].tolist()
 
 
@@ -134,6 +136,52 @@ def test_moving_object_distance_vs_oracle(oracle):
         got = host.MovingObjectDistanceCalculator(side, t_this, this, cur, old, older, tri, t_cur, t_old, t_older)
         ref = _oracle_mo(oracle, side, t_this, this, cur, old, older, tri, t_cur, t_old, t_older)
         assert _same(got, ref), (trial, got, ref)
+
+
+def test_moving_object_distance_caller_interp_vs_oracle(oracle):
+    """A non-empty caller InterpolatedVectorCenter_pointOtherCamera, shorter and longer than the
+    triple list: triple i is measured against element i of the grown by-value copy
+    (P/DistanceCalculator.cpp:19,67,75-80) -- the caller's point while i < n, else the point
+    extrapolated at iteration i - n."""
+    rng = np.random.default_rng(12)
+    for trial in range(3000):
+        pts = lambda n: (rng.random((n, 2)) * [640, 480]).astype(np.float32)  # noqa: E731
+        nthis, ncur, nold, nolder = (int(rng.integers(0, 7)) for _ in range(4))
+        this, cur, old, older = pts(nthis), pts(ncur), pts(nold), pts(nolder)
+        ntri = int(rng.integers(0, 8))
+        tri = rng.integers(-1, 7, (ntri, 3)).astype(np.int32)
+        interp = pts(int(rng.integers(1, 9)))
+        base = int(rng.integers(10**9, 10**12))
+        t_older = base
+        t_old = t_older + int(rng.integers(1, 80_000_000))
+        t_cur = t_old + int(rng.integers(1, 80_000_000))
+        t_this = t_cur + int(rng.integers(-40_000_000, 40_000_000))
+        side = bool(rng.integers(0, 2))
+        got, grown = host.MovingObjectDistanceCalculator(side, t_this, this, cur, old, older, tri, t_cur, t_old,
+                                                         t_older, return_interpolated=True, interpolated=interp)
+        ref = _oracle_mo(oracle, side, t_this, this, cur, old, older, tri, t_cur, t_old, t_older, interp)
+        assert _same(got, ref), (trial, got, ref)
+        assert np.array_equal(grown[:len(interp)], interp)
+        assert len(grown) == len(interp) + len(got)
+
+
+def test_moving_object_distance_caller_interp_known_answer(oracle):
+    """Static other-camera object at (290, 100); this camera sees (300, 100) and (400, 100).
+    Caller vector [(250, 100)] (one point, two triples): triple 0 is measured against (250, 100)
+    -> disp 50; triple 1 against the point pushed at iteration 0, (290, 100) -> disp 110.
+    With an empty caller vector the disparities are 10 and 110."""
+    lut = distance_lut_cm()
+    args = (True, 3_000_000, [(300.0, 100.0), (400.0, 100.0)], [(290.0, 100.0)], [(290.0, 100.0)],
+            [(290.0, 100.0)], [(0, 0, 0), (0, 0, 0)], 2_000_000, 1_000_000, 0)
+    assert host.MovingObjectDistanceCalculator(*args) == [lut[10], lut[110]]
+    got, grown = host.MovingObjectDistanceCalculator(*args, return_interpolated=True, interpolated=[(250.0, 100.0)])
+    assert got == [lut[50], lut[110]]
+    assert grown.tolist() == [[250.0, 100.0], [290.0, 100.0], [290.0, 100.0]]
+    assert _oracle_mo(oracle, *args, interp=[(250.0, 100.0)]) == got
+    # longer than the triple list: only the caller's points are read
+    got = host.MovingObjectDistanceCalculator(*args, interpolated=[(250.0, 100.0), (380.0, 100.0), (0.0, 0.0)])
+    assert got == [lut[50], lut[20]]
+    assert _oracle_mo(oracle, *args, interp=[(250.0, 100.0), (380.0, 100.0), (0.0, 0.0)]) == got
 
 
 def test_moving_object_distance_static_scene():

@@ -37,6 +37,14 @@ def test_distance_path(cpp_out):
                                               [(0, 0, 0), (1, 1, 1), (5, 0, 0)], 1033000000, 1000000000,
                                               966000000)
     assert cpp_out["dist"] == ref and len(ref) == 3
+    interps = [[(250.0, 190.0)], [(250.0, 190.0), (60.0, 40.0), (1.0, 2.0), (3.0, 4.0), (5.0, 6.0)]]
+    for k, interp in enumerate(interps):
+        ref_k = host.MovingObjectDistanceCalculator(True, 1040000000, this, [(300, 201), (80.5, 49)],
+                                                    [(298, 200), (79, 48.5)], [(297, 199.5), (78, 48)],
+                                                    [(0, 0, 0), (1, 1, 1), (5, 0, 0)], 1033000000, 1000000000,
+                                                    966000000, interpolated=interp)
+        assert cpp_out[f"dist_interp{k}"] == ref_k and len(ref_k) == 3
+        assert ref_k[0] != ref[0]  # triple 0 is measured against the caller's point, not its own
     assert cpp_out["pos_off"] == 0
     pos = host.CooridinatePositionCalculator(False, ref, this, True)
     assert [list(p) for p in pos] == cpp_out["pos"] or all(

@@ -74,6 +74,7 @@ SIGNATURES = {
                                     POINTER(c_float), POINTER(c_int)]),
     "usv_moving_object_distance": (c_int, [c_int, c_int64, POINTER(c_float), c_int, POINTER(c_float),
                                            c_int, POINTER(c_float), c_int, POINTER(c_float), c_int,
+                                           POINTER(c_float), c_int,
                                            POINTER(c_int), c_int, c_int64, c_int64, c_int64,
                                            POINTER(c_double), POINTER(c_float), POINTER(c_int)]),
     "usv_coordinate_position": (c_int, [c_int, POINTER(c_double), c_int, POINTER(c_float), c_int, c_int,

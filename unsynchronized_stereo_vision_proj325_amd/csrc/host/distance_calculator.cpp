@@ -168,12 +168,14 @@ extern "C" usv_status usv_distance_lut_cm(int model, double* lut_out) {
 extern "C" usv_status usv_moving_object_distance(
     int camera_side_left, int64_t ts_this, const float* this_pts, int n_this, const float* cur_pts,
     int n_cur, const float* old_pts, int n_old, const float* older_pts, int n_older,
-    const int* triples, int n_triples, int64_t ts_other, int64_t ts_other_old,
-    int64_t ts_other_older, double* dist_out, float* interp_out, int* n_out) {
-    if (!n_out || n_this < 0 || n_cur < 0 || n_old < 0 || n_older < 0 || n_triples < 0)
+    const float* interp_in, int n_interp_in, const int* triples, int n_triples, int64_t ts_other,
+    int64_t ts_other_old, int64_t ts_other_older, double* dist_out, float* interp_out, int* n_out) {
+    if (!n_out || n_this < 0 || n_cur < 0 || n_old < 0 || n_older < 0 || n_triples < 0 ||
+        n_interp_in < 0)
         return USV_ERR_INVALID_ARG;
     if ((n_this && !this_pts) || (n_cur && !cur_pts) || (n_old && !old_pts) ||
-        (n_older && !older_pts) || (n_triples && (!triples || !dist_out)))
+        (n_older && !older_pts) || (n_interp_in && !interp_in) ||
+        (n_triples && (!triples || !dist_out)))
         return USV_ERR_INVALID_ARG;
     auto pts = [](const float* p, int n) {
         std::vector<Point2f> v;
@@ -187,7 +189,8 @@ extern "C" usv_status usv_moving_object_distance(
     using tp = steady_clock::time_point;
     auto at = [](int64_t ns) { return tp(std::chrono::duration_cast<steady_clock::duration>(std::chrono::nanoseconds(ns))); };
     std::vector<double> dist;
-    std::vector<Point2f> interp;  // the reference's caller passes an empty vector (P/Main.cpp:869-871)
+    // the reference's caller passes an empty vector (P/Main.cpp:869-871); any other is honoured
+    std::vector<Point2f> interp = pts(interp_in, n_interp_in);
     usv::moving_object_distance(camera_side_left != 0, at(ts_this), pts(this_pts, n_this),
                                 pts(cur_pts, n_cur), pts(old_pts, n_old), pts(older_pts, n_older),
                                 interp, tri, at(ts_other), at(ts_other_old), at(ts_other_older), dist);

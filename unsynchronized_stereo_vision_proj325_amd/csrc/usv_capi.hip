@@ -4,7 +4,10 @@
 // (lane-per-disparity) or generic kernel.  No allocation, no synchronisation:
 // everything is enqueued on the caller's stream, so a caller may capture these
 // calls in a hipGraph.
+#include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "usv.h"
 #include "usv_kernels.hpp"
@@ -12,6 +15,65 @@
 namespace {
 
 usv_status to_status(hipError_t e) { return e == hipSuccess ? USV_OK : USV_ERR_HIP; }
+
+// ---- distance tables given in host memory -----------------------------------
+// The kernels read the 256-entry table on the device.  A caller may pass a
+// device pointer (used as is), a pinned/registered host pointer (its device
+// alias is used) or ordinary pageable host memory, e.g. the
+// `static double lut[256]` that usv_distance_lut_cm fills.
+// Pageable tables are copied once per (device, contents) into a library-owned
+// device buffer that lives until process exit; later calls with the same
+// contents find it by value and enqueue nothing extra.  The first call with a
+// new table copies it synchronously (hipMemcpy), so make that call once before
+// capturing a hipGraph.  Bounded: at most kMaxHostTables distinct tables.
+struct HostTable {
+    int device;
+    double values[256];
+    double* dev;
+};
+constexpr size_t kMaxHostTables = 64;
+std::mutex g_tables_mu;
+std::vector<HostTable*> g_tables;
+
+usv_status resolve_lut(const double* lut, const double** dev_lut) {
+    *dev_lut = lut;
+    if (!lut) return USV_OK;
+    hipPointerAttribute_t attr{};
+    hipError_t e = hipPointerGetAttributes(&attr, lut);
+    if (e == hipSuccess && (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged ||
+                            attr.type == hipMemoryTypeUnified)) {
+        return USV_OK;
+    }
+    if (e == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer) {
+        *dev_lut = static_cast<const double*>(attr.devicePointer);  // pinned / registered host memory
+        return USV_OK;
+    }
+    (void)hipGetLastError();  // an unregistered pointer may leave an error behind; clear it
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return USV_ERR_HIP;
+    std::lock_guard<std::mutex> lock(g_tables_mu);
+    for (const HostTable* t : g_tables)
+        if (t->device == device && std::memcmp(t->values, lut, sizeof(t->values)) == 0) {
+            *dev_lut = t->dev;
+            return USV_OK;
+        }
+    if (g_tables.size() >= kMaxHostTables) return USV_ERR_UNSUPPORTED;
+    auto* t = new HostTable{};
+    t->device = device;
+    std::memcpy(t->values, lut, sizeof(t->values));
+    if (hipMalloc(&t->dev, sizeof(t->values)) != hipSuccess) {
+        delete t;
+        return USV_ERR_HIP;
+    }
+    if (hipMemcpy(t->dev, t->values, sizeof(t->values), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(t->dev);
+        delete t;
+        return USV_ERR_HIP;
+    }
+    g_tables.push_back(t);
+    *dev_lut = t->dev;
+    return USV_OK;
+}
 
 usv_status validate(const usv::MatchArgs& a) {
     if (!a.L || !a.R || !a.disp) return USV_ERR_INVALID_ARG;
@@ -28,9 +90,13 @@ usv_status validate(const usv::MatchArgs& a) {
     return USV_OK;
 }
 
-usv_status dispatch(const usv::MatchArgs& a, int kernel, void* stream) {
+usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
     usv_status st = validate(a);
     if (st != USV_OK) return st;
+    if (kernel != USV_KERNEL_AUTO && kernel != USV_KERNEL_FAST && kernel != USV_KERNEL_GENERIC)
+        return USV_ERR_INVALID_ARG;
+    if (kernel == USV_KERNEL_FAST && !usv::fast_path_supported(a)) return USV_ERR_UNSUPPORTED;
+    if (a.dist && (st = resolve_lut(a.lut, &a.lut)) != USV_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (kernel) {
         case USV_KERNEL_AUTO:
@@ -96,6 +162,8 @@ usv_status usv_disparity_to_distance(const uint8_t* disp, int W, int H, int disp
                                      const double* lut_cm, double* out, int out_pitch, void* stream) {
     if (!disp || !lut_cm || !out || W <= 0 || H <= 0 || disp_pitch < W || out_pitch < W)
         return USV_ERR_INVALID_ARG;
+    usv_status st = resolve_lut(lut_cm, &lut_cm);
+    if (st != USV_OK) return st;
     return to_status(usv::launch_disp_to_dist(disp, W, H, disp_pitch, lut_cm, out, out_pitch,
                                               static_cast<hipStream_t>(stream)));
 }

@@ -116,27 +116,33 @@ def _f32(pts):
 
 def MovingObjectDistanceCalculator(camera_side_left, ts_this, this_pts, cur_pts, old_pts, older_pts,
                                    triples, ts_other, ts_other_old, ts_other_older,
-                                   return_interpolated=False):
-    """Time stamps are steady_clock ticks (ns).  Returns the appended dist list (cm)."""
+                                   return_interpolated=False, interpolated=()):
+    """Time stamps are steady_clock ticks (ns).  Returns the appended dist list (cm).
+
+    `interpolated` is the caller's InterpolatedVectorCenter_pointOtherCamera (by value in the
+    reference, normally empty); with return_interpolated the grown vector (those points, then one
+    extrapolated point per triple, P/DistanceCalculator.cpp:67) is returned as well."""
     lib = _lib.load()
     t, nt = _f32(this_pts)
     c, nc = _f32(cur_pts)
     o, no = _f32(old_pts)
     q, nq = _f32(older_pts)
+    ii, ni = _f32(interpolated) if len(interpolated) else (np.zeros(2, np.float32), 0)
     tri = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1))
     ntri = len(tri) // 3
     dist = np.zeros(max(ntri, 1), dtype=np.float64)
-    interp = np.zeros(2 * max(ntri, 1), dtype=np.float32)
+    interp = np.zeros(2 * max(ni + ntri, 1), dtype=np.float32)
     n = c_int(0)
     fp, ip, dp = POINTER(c_float), POINTER(c_int), POINTER(c_double)
     _lib.check("usv_moving_object_distance", lib.usv_moving_object_distance(
         int(bool(camera_side_left)), int(ts_this), t.ctypes.data_as(fp), nt, c.ctypes.data_as(fp), nc,
-        o.ctypes.data_as(fp), no, q.ctypes.data_as(fp), nq, tri.ctypes.data_as(ip), ntri,
+        o.ctypes.data_as(fp), no, q.ctypes.data_as(fp), nq, ii.ctypes.data_as(fp), ni,
+        tri.ctypes.data_as(ip), ntri,
         int(ts_other), int(ts_other_old), int(ts_other_older), dist.ctypes.data_as(dp),
         interp.ctypes.data_as(fp), ctypes.byref(n)))
     d = dist[:n.value].tolist()
     if return_interpolated:
-        return d, interp[:2 * n.value].reshape(-1, 2)
+        return d, interp[:2 * (ni + n.value)].reshape(-1, 2)
     return d
 
 
