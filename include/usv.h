@@ -18,8 +18,9 @@
  *                             motion mask absdiff at P/Main.cpp:304 and its
  *                             "disparity" is a centroid x-difference
  *                             (P/DistanceCalculator.cpp:69-81, P/Main.cpp:681-693).
- *   usv_distance_lut_cm       P/DistanceCalculator.cpp:84 (model 0) and
- *                             P/Main.cpp:694 (model 1), tabulated for d=0..255.
+ *   usv_distance_lut_cm/_mm   P/DistanceCalculator.cpp:84 (model 0) and
+ *                             P/Main.cpp:694 (model 1), tabulated for d=0..255
+ *                             (cm as the reference prints, P/Main.cpp:1265; mm = 10 cm).
  *   usv_disparity_to_distance per-pixel form of P/DistanceCalculator.cpp:84
  *                             (SURVEY.md §8(a) A11).
  *   usv_moving_object_distance  array form of MovingObjectDistanceCalculator,
@@ -68,7 +69,8 @@ typedef enum {
     USV_ERR_INVALID_ARG = 1,  /* null pointer, bad size, pitch < width, ... */
     USV_ERR_UNSUPPORTED = 2,  /* parameter outside the engine's range (D > 256, even w, ...) */
     USV_ERR_HIP = 3,          /* a HIP runtime call failed (launch, copy) */
-    USV_ERR_NO_DEVICE = 4     /* no gfx950 device visible */
+    USV_ERR_NO_DEVICE = 4,    /* no gfx950 device visible */
+    USV_ERR_COMM = 5          /* an RCCL call failed (multi-GPU engine) */
 } usv_status;
 
 typedef enum { USV_METRIC_SAD = 0, USV_METRIC_SSD = 1 } usv_metric;
@@ -129,8 +131,57 @@ usv_status usv_sad_disparity_batch(const uint8_t* L, const uint8_t* R, int batch
                                    int disp_pitch, double* dist_cm, size_t dist_stride,
                                    int dist_pitch, const double* lut_cm, void* stream);
 
+/* ---- multi-GPU: one process, one device + stream + RCCL communicator per GPU ----
+ *
+ * SURVEY.md §8(b)(2) / §8(e).  A batch of independent frame pairs (configs D
+ * and E: 8 pairs over 8 GPUs) is split into contiguous shards (usv_shard_range:
+ * pair i -> GPU i when batch == n), each GPU matches its shard with the
+ * batched kernel, and ONE ncclGather (rccl.h:745) brings the u8 disparity maps
+ * to devices[0]; the distance maps are expanded there from the 256-entry table
+ * (never shipped).  Replaces nothing in the reference (its two camera threads,
+ * P/Main.cpp:1407-1420, share one CPU); it is the entry a C++ caller uses to
+ * shard frames over the node.  Not thread-safe per engine: one caller at a time.
+ */
+typedef struct usv_sharded_engine usv_sharded_engine;
+
+/* HOST: shard [*first, *first + *count) of a batch of `batch` pairs for GPU k of n. */
+usv_status usv_shard_range(int batch, int n_devices, int k, int* first, int* count);
+
+/* Engine for up to max_pairs W x H pairs per call on the n_devices listed GPUs
+ * (distinct HIP ordinals; devices[0] is the gather root).  Allocates each GPU's
+ * dense input / output shard buffers (ceil(max_pairs / n) pairs, pitch W) and
+ * calls ncclCommInitAll.  USV_ERR_NO_DEVICE without a GPU. */
+usv_status usv_sharded_create(const int* devices, int n_devices, int max_pairs, int W, int H, int D, int w,
+                              int metric, usv_sharded_engine** out);
+usv_status usv_sharded_destroy(usv_sharded_engine* e);
+
+/* DEVICE buffers of GPU k's shard inputs (dense, pitch W, pair j at j*W*H):
+ * fill them and pass L = R = NULL to usv_batch_sharded to match HBM-resident frames. */
+usv_status usv_sharded_input_buffers(usv_sharded_engine* e, int k, uint8_t** L, uint8_t** R);
+
+/* DEVICE results on devices[0] after usv_batch_sharded: the gather buffer
+ * (GPU k's shard at slot k, i.e. k * ceil(max_pairs / n) * W * H bytes; equal
+ * to batch order when batch == n * ceil(max_pairs / n)) and the distance maps
+ * in batch order (NULL until a call asked for them). */
+usv_status usv_sharded_outputs(usv_sharded_engine* e, const uint8_t** disp, const double** dist_cm);
+
+/* Match a batch (1 <= batch <= max_pairs) across the engine's GPUs.  BLOCKING:
+ * returns when the results are in place.
+ *   L, R      : HOST batch (pair b at L + b * pair_stride, row pitch `pitch`),
+ *               or both NULL = the frames already sit in usv_sharded_input_buffers.
+ *   disp      : nullable HOST output, batch x H x W dense u8, batch order.
+ *   dist_cm   : nullable HOST output, batch x H x W doubles; with_distance != 0
+ *               computes the maps on devices[0] even when dist_cm is NULL.
+ *   lut_cm    : the 256-entry table (host or device) when distances are wanted.
+ * The calling thread's current device is restored before returning. */
+usv_status usv_batch_sharded(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int batch,
+                             size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
+                             const double* lut_cm, int with_distance);
+
 /* HOST: lut_out[d] = distance(d) in cm for d = 0..255 (d = 0 -> +inf for model 0). */
 usv_status usv_distance_lut_cm(int model, double* lut_out);
+/* HOST: the same table in mm (north_star's unit): lut_out[d] = 10 * cm(d). */
+usv_status usv_distance_lut_mm(int model, double* lut_out);
 
 /* DEVICE: out[y*out_pitch + x] = lut_cm[disp[y*disp_pitch + x]] (doubles);
  * lut_cm in device or host memory, as for usv_sad_disparity_ex. */

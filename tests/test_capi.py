@@ -3,6 +3,7 @@ symbol, validates arguments without touching a GPU, and its host object path
 (the C++ restatements behind Match.hpp / DistanceCalculator.hpp /
 Matching.hpp) agrees bit for bit with the oracle."""
 import ctypes
+import json
 import math
 import os
 import re
@@ -12,7 +13,7 @@ import pytest
 
 from oracle_lib import REF_MATCH_PATH, oracle_match
 from unsynchronized_stereo_vision_proj325_amd import _lib, host
-from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm
+from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm, distance_lut_mm
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
@@ -68,6 +69,21 @@ def test_distance_lut_bitexact(oracle, model):
     for d in range(256):
         ref = f(d)
         assert (lut[d] == ref) or (math.isinf(lut[d]) and math.isinf(ref)), (d, lut[d], ref)
+
+
+@pytest.mark.parametrize("model", ["moving_object", "canny"])
+def test_distance_lut_mm(model):
+    """mm table = 10 x the cm table, pinned against the SURVEY §8(c) golden cm values; north_star's
+    1e-4 relative tolerance on mm is met with margin (one double rounding)."""
+    cm, mm = distance_lut_cm(model), distance_lut_mm(model)
+    assert np.array_equal(mm, cm * 10.0)
+    if model == "moving_object":
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_golden.json")))
+        for d, v in gold["distance_cm"]["values"]:
+            if v == "inf":
+                assert math.isinf(mm[d])
+            else:
+                assert abs(mm[d] - 10 * float(v)) <= 1e-12 * mm[d], (d, mm[d], v)
 
 
 def _rand_matches(rng, n, nl, nr):

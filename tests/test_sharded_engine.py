@@ -1,0 +1,107 @@
+"""The C-ABI multi-GPU engine (include/usv.h usv_sharded_*, csrc/usv_sharded.hip).
+
+CPU: the shard partition equals sharding.pair_range, argument validation, and a
+clean USV_ERR_NO_DEVICE without a GPU.  GPU: config D's per-node workload (8
+1080p pairs, w=11, D=128) through usv_batch_sharded on the box's GPU(s) --
+RCCL communicator, batched kernel and ncclGather included -- bit-exact against
+the oracle, host-buffer and HBM-resident forms, distance maps on the root.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle_lib import oracle_sad
+from unsynchronized_stereo_vision_proj325_amd import _lib
+from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm
+from unsynchronized_stereo_vision_proj325_amd.sharding import ShardedMatcher, pair_range
+from unsynchronized_stereo_vision_proj325_amd.synthetic import synthetic_pair
+
+
+def test_shard_range_equals_pair_range(usvlib):
+    first, count = ctypes.c_int(), ctypes.c_int()
+    for batch in range(0, 40):
+        for n in range(1, 10):
+            covered = []
+            for k in range(n):
+                assert usvlib.usv_shard_range(batch, n, k, ctypes.byref(first), ctypes.byref(count)) == _lib.USV_OK
+                assert (first.value, first.value + count.value) == pair_range(batch, k, n)
+                covered += list(range(first.value, first.value + count.value))
+            assert covered == list(range(batch))
+    assert usvlib.usv_shard_range(4, 0, 0, ctypes.byref(first), ctypes.byref(count)) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_shard_range(4, 2, 2, ctypes.byref(first), ctypes.byref(count)) == _lib.USV_ERR_INVALID_ARG
+
+
+def test_sharded_create_validation_no_gpu(usvlib):
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 1)
+    assert usvlib.usv_sharded_create(devs, 2, 8, 64, 64, 300, 5, 0, ctypes.byref(h)) == _lib.USV_ERR_UNSUPPORTED
+    assert usvlib.usv_sharded_create(devs, 0, 8, 64, 64, 16, 5, 0, ctypes.byref(h)) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_sharded_create(devs, 2, 0, 64, 64, 16, 5, 0, ctypes.byref(h)) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_batch_sharded(None, None, None, 1, 0, 64, None, None, None, 0) == _lib.USV_ERR_INVALID_ARG
+    import torch
+    if not torch.cuda.is_available():
+        assert usvlib.usv_sharded_create(devs, 1, 8, 64, 64, 16, 5, 0, ctypes.byref(h)) == _lib.USV_ERR_NO_DEVICE
+        assert not h.value
+
+
+@pytest.mark.gpu
+def test_batch_sharded_config_d_host_buffers(gpu):
+    import torch
+    n = torch.cuda.device_count()
+    W, H, D, w, B = 1920, 1080, 128, 11, 8
+    pairs = [synthetic_pair(W, H, D, pair_index=60 + i, noise=2) for i in range(B)]
+    L = np.stack([p[0] for p in pairs])
+    R = np.stack([p[1] for p in pairs])
+    eng = ShardedMatcher(list(range(n)), B, W, H, D, w)
+    try:
+        disp, dist = eng.run(L, R, with_distance=True)
+        lut = distance_lut_cm()
+        for i, (l, r, _) in enumerate(pairs):
+            assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), i
+        assert np.array_equal(dist, lut[disp])
+        # ragged batch (fewer pairs than max_pairs): shards shrink, order kept
+        disp5, _ = eng.run(L[:5], R[:5])
+        assert np.array_equal(disp5, disp[:5])
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_batch_sharded_resident_inputs(gpu):
+    """Frames already in HBM (usv_sharded_input_buffers), results read from the root's gather buffer."""
+    import torch
+    W, H, D, w, B = 640, 480, 64, 7, 4
+    pairs = [synthetic_pair(W, H, D, pair_index=70 + i) for i in range(B)]
+    eng = ShardedMatcher([0], B, W, H, D, w)
+    try:
+        Lp, Rp = eng.input_buffers(0)
+        frame = W * H
+        for i, (l, r, _) in enumerate(pairs):
+            for ptr, img in ((Lp, l), (Rp, r)):
+                src = torch.from_numpy(np.ascontiguousarray(img).reshape(-1)).to("cuda:0")
+                _copy_to_device(ptr + i * frame, src)
+        disp, _ = eng.run(batch=B, with_distance=True)
+        dptr, xptr = eng.outputs()
+        assert dptr and xptr
+        got = _copy_from_device(dptr, B * frame).reshape(B, H, W)
+        assert np.array_equal(got, disp)
+        for i, (l, r, _) in enumerate(pairs):
+            assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), i
+    finally:
+        eng.close()
+
+
+def _copy_to_device(ptr, src):
+    import torch
+    lib = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.synchronize()
+    assert lib.hipMemcpy(ctypes.c_void_p(ptr), ctypes.c_void_p(src.data_ptr()), ctypes.c_size_t(src.numel()),
+                         3) == 0  # hipMemcpyDeviceToDevice
+
+
+def _copy_from_device(ptr, n):
+    lib = ctypes.CDLL("libamdhip64.so")
+    out = np.empty(n, np.uint8)
+    assert lib.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), ctypes.c_size_t(n), 2) == 0
+    return out

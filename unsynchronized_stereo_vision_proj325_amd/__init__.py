@@ -10,7 +10,8 @@ include/usv.h); this package is the Python host layer used by tests and bench.
 """
 from . import _lib  # noqa: F401
 from .calibration import CalibrationDataParameters, load_calibration, save_calibration  # noqa: F401
-from .engine import StereoBlockMatcher, disparity_to_distance, distance_lut_cm, sad_disparity  # noqa: F401
+from .engine import (StereoBlockMatcher, disparity_to_distance, distance_lut_cm, distance_lut_mm,  # noqa: F401
+                     sad_disparity)
 
 __all__ = ["StereoBlockMatcher", "sad_disparity", "disparity_to_distance", "distance_lut_cm",
            "CalibrationDataParameters", "load_calibration", "save_calibration"]

@@ -20,12 +20,14 @@ USV_ERR_INVALID_ARG = 1
 USV_ERR_UNSUPPORTED = 2
 USV_ERR_HIP = 3
 USV_ERR_NO_DEVICE = 4
+USV_ERR_COMM = 5
 STATUS_NAMES = {
     USV_OK: "USV_OK",
     USV_ERR_INVALID_ARG: "USV_ERR_INVALID_ARG",
     USV_ERR_UNSUPPORTED: "USV_ERR_UNSUPPORTED",
     USV_ERR_HIP: "USV_ERR_HIP",
     USV_ERR_NO_DEVICE: "USV_ERR_NO_DEVICE",
+    USV_ERR_COMM: "USV_ERR_COMM",
 }
 
 METRIC_SAD, METRIC_SSD = 0, 1
@@ -56,7 +58,16 @@ SIGNATURES = {
     "usv_sad_disparity_batch": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_void_p, c_size_t, c_int, c_void_p,
                                         c_size_t, c_int, c_void_p, c_void_p]),
+    "usv_shard_range": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
+    "usv_sharded_create": (c_int, [POINTER(c_int), c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   POINTER(c_void_p)]),
+    "usv_sharded_destroy": (c_int, [c_void_p]),
+    "usv_sharded_input_buffers": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_void_p)]),
+    "usv_sharded_outputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "usv_batch_sharded": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_size_t, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_int]),
     "usv_distance_lut_cm": (c_int, [c_int, POINTER(c_double)]),
+    "usv_distance_lut_mm": (c_int, [c_int, POINTER(c_double)]),
     "usv_disparity_to_distance": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                           c_void_p]),
     "usv_resolve_match_list": (c_int, [POINTER(usv_match), c_int, POINTER(usv_match), POINTER(c_int)]),

@@ -165,6 +165,15 @@ extern "C" usv_status usv_distance_lut_cm(int model, double* lut_out) {
     return USV_OK;
 }
 
+// north_star quotes distance in mm: the same table times 10 (one double multiply per entry, so
+// mm[d] / 10 is cm[d] to within one rounding; inf stays inf).
+extern "C" usv_status usv_distance_lut_mm(int model, double* lut_out) {
+    usv_status st = usv_distance_lut_cm(model, lut_out);
+    if (st != USV_OK) return st;
+    for (int d = 0; d < 256; ++d) lut_out[d] = lut_out[d] * 10.0;
+    return USV_OK;
+}
+
 extern "C" usv_status usv_moving_object_distance(
     int camera_side_left, int64_t ts_this, const float* this_pts, int n_this, const float* cur_pts,
     int n_cur, const float* old_pts, int n_old, const float* older_pts, int n_older,

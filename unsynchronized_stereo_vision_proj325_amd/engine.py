@@ -37,6 +37,33 @@ def distance_lut_cm(model: str = "moving_object") -> np.ndarray:
     return out
 
 
+def distance_lut_mm(model: str = "moving_object") -> np.ndarray:
+    """The same table in mm (north_star's unit): lut_mm[d] = 10 * lut_cm[d] (usv_distance_lut_mm)."""
+    lib = _lib.load()
+    out = np.empty(256, dtype=np.float64)
+    _lib.check("usv_distance_lut_mm",
+               lib.usv_distance_lut_mm(_MODELS[model], out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+    return out
+
+
+_UNITS = {"cm": distance_lut_cm, "mm": distance_lut_mm}
+# (model, unit, device index) -> device copy of the table; built once, never freed, so no launch
+# ever has to wait for (or synchronise on) a temporary table
+_LUT_CACHE: dict[tuple[str, str, int], torch.Tensor] = {}
+
+
+def lut_device(model: str, unit: str, device: torch.device) -> torch.Tensor:
+    """Device copy of the distance table for (model, unit), cached per device."""
+    if model not in _MODELS or unit not in _UNITS:
+        raise ValueError(f"model must be one of {sorted(_MODELS)}, unit one of {sorted(_UNITS)}")
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (model, unit, idx)
+    if key not in _LUT_CACHE:
+        _LUT_CACHE[key] = torch.from_numpy(_UNITS[unit](model)).to(torch.device("cuda", idx))
+        torch.cuda.synchronize(idx)  # the copy is complete before any stream may read the table
+    return _LUT_CACHE[key]
+
+
 def _stream(stream) -> int:
     s = torch.cuda.current_stream() if stream is None else stream
     return s.cuda_stream
@@ -64,19 +91,20 @@ class StereoBlockMatcher:
     metric: str = "sad"
     distance_model: str = "moving_object"
     kernel: str = "auto"
+    distance_unit: str = "cm"
 
     def __post_init__(self):
         if self.metric not in _METRICS:
             raise ValueError(f"metric must be one of {sorted(_METRICS)}")
         if self.kernel not in _KERNELS:
             raise ValueError(f"kernel must be one of {sorted(_KERNELS)}")
-        self._lut_dev: dict[int, torch.Tensor] = {}
+        if self.distance_model not in _MODELS:
+            raise ValueError(f"distance_model must be one of {sorted(_MODELS)}")
+        if self.distance_unit not in _UNITS:
+            raise ValueError(f"distance_unit must be one of {sorted(_UNITS)}")
 
     def lut_device(self, device: torch.device) -> torch.Tensor:
-        key = device.index if device.index is not None else torch.cuda.current_device()
-        if key not in self._lut_dev:
-            self._lut_dev[key] = torch.from_numpy(distance_lut_cm(self.distance_model)).to(device)
-        return self._lut_dev[key]
+        return lut_device(self.distance_model, self.distance_unit, device)
 
     def compute(self, left: torch.Tensor, right: torch.Tensor, *, with_distance: bool = False,
                 out_disp: torch.Tensor | None = None, out_dist: torch.Tensor | None = None,
@@ -96,6 +124,8 @@ class StereoBlockMatcher:
         _check_image(out_disp, "out_disp")
         if tuple(out_disp.shape) != tuple(left.shape):
             raise ValueError("out_disp shape mismatch")
+        if out_disp.device != left.device:
+            raise ValueError("out_disp must be on the same device as left/right")
         lut = None
         if with_distance:
             lut = self.lut_device(left.device)
@@ -104,6 +134,8 @@ class StereoBlockMatcher:
             if out_dist.dtype != torch.float64 or tuple(out_dist.shape) != tuple(left.shape) \
                     or out_dist.stride(-1) != 1 or not out_dist.is_cuda:
                 raise ValueError("out_dist must be a float64 CUDA tensor shaped like left")
+            if out_dist.device != left.device:
+                raise ValueError("out_dist must be on the same device as left/right")
         lib = _lib.load()
         with torch.cuda.device(left.device):
             s = _stream(stream)
@@ -138,20 +170,22 @@ def sad_disparity(left: torch.Tensor, right: torch.Tensor, num_disparities: int,
 
 
 def disparity_to_distance(disp: torch.Tensor, model: str = "moving_object",
-                          out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """Per-pixel distance map (cm, float64) of a u8 disparity map."""
+                          out: torch.Tensor | None = None, stream=None, unit: str = "cm") -> torch.Tensor:
+    """Per-pixel distance map (float64, cm or mm) of a u8 disparity map.
+    Stream-ordered, no host synchronisation: the table is the cached per-device copy."""
     _check_image(disp, "disp")
     if disp.dim() != 2:
         raise ValueError("disparity_to_distance takes one (H, W) map")
     H, W = disp.shape
     if out is None:
         out = torch.empty((H, W), dtype=torch.float64, device=disp.device)
-    lut = torch.from_numpy(distance_lut_cm(model)).to(disp.device)
+    if out.dtype != torch.float64 or tuple(out.shape) != (H, W) or out.stride(-1) != 1 \
+            or out.device != disp.device:
+        raise ValueError("out must be a float64 (H, W) tensor on disp's device")
+    lut = lut_device(model, unit, disp.device)
     lib = _lib.load()
     with torch.cuda.device(disp.device):
         _lib.check("usv_disparity_to_distance",
                    lib.usv_disparity_to_distance(disp.data_ptr(), W, H, disp.stride(0), lut.data_ptr(),
                                                  out.data_ptr(), out.stride(0), _stream(stream)))
-    # keep lut alive until the kernel has consumed it
-    (torch.cuda.current_stream() if stream is None else stream).synchronize()
     return out

@@ -118,3 +118,79 @@ def gather_bands(local, H: int, dst: int = 0, group=None, recv: list | None = No
     if rank != dst:
         return None
     return torch.cat([bufs[r][:pair_range(H, r, world)[1] - pair_range(H, r, world)[0]] for r in range(world)], 0)
+
+
+# ---- one process, several GPUs: the C-ABI engine (include/usv.h usv_sharded_*) ----
+
+class ShardedMatcher:
+    """usv_sharded_engine through ctypes: one process drives `devices` (HIP ordinals), one stream and
+    RCCL communicator per GPU; pairs shard like pair_range and one ncclGather brings the u8 maps to
+    devices[0] (csrc/usv_sharded.hip).  This is the entry the reference's single C++ process would use;
+    bench.py's one-process-per-GPU torch.distributed path is the other form of the same split."""
+
+    def __init__(self, devices, max_pairs: int, W: int, H: int, D: int, w: int, metric: str = "sad"):
+        import ctypes
+
+        from . import _lib
+        self._ct, self._lib_mod = ctypes, _lib
+        self.lib = _lib.load()
+        self.devices = list(devices)
+        self.W, self.H, self.max_pairs = W, H, max_pairs
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _lib.check("usv_sharded_create", self.lib.usv_sharded_create(
+            devs, len(self.devices), max_pairs, W, H, D, w, {"sad": 0, "ssd": 1}[metric], ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self._lib_mod.check("usv_sharded_destroy", self.lib.usv_sharded_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def input_buffers(self, k: int):
+        """Device pointers (L, R) of GPU k's dense shard inputs."""
+        ct = self._ct
+        L, R = ct.c_void_p(), ct.c_void_p()
+        self._lib_mod.check("usv_sharded_input_buffers",
+                            self.lib.usv_sharded_input_buffers(self.handle, k, ct.byref(L), ct.byref(R)))
+        return L.value, R.value
+
+    def outputs(self):
+        """Device pointers (gathered u8 disparity on devices[0], distance maps or None)."""
+        ct = self._ct
+        d, x = ct.c_void_p(), ct.c_void_p()
+        self._lib_mod.check("usv_sharded_outputs", self.lib.usv_sharded_outputs(self.handle, ct.byref(d),
+                                                                                 ct.byref(x)))
+        return d.value, x.value
+
+    def run(self, L=None, R=None, batch: int | None = None, with_distance: bool = False, lut=None,
+            want_host: bool = True):
+        """Host numpy batches (B, H, W) u8 -> (disp (B, H, W) u8, dist (B, H, W) f64 or None), or with
+        L = R = None the frames already in input_buffers (then `batch` is required)."""
+        import numpy as np
+        ct = self._ct
+        if L is not None:
+            L = np.ascontiguousarray(L)
+            R = np.ascontiguousarray(R)
+            if L.shape != R.shape or L.ndim != 3 or L.shape[1:] != (self.H, self.W) or L.dtype != np.uint8:
+                raise ValueError("L, R must be (B, H, W) uint8 batches of the engine's geometry")
+            batch = L.shape[0]
+        if batch is None:
+            raise ValueError("batch is required for resident inputs")
+        disp = np.empty((batch, self.H, self.W), np.uint8) if want_host else None
+        dist = np.empty((batch, self.H, self.W), np.float64) if (with_distance and want_host) else None
+        if with_distance and lut is None:
+            from .engine import distance_lut_cm
+            lut = distance_lut_cm()
+        lut_arr = np.ascontiguousarray(lut, dtype=np.float64) if lut is not None else None
+        vp = lambda a: a.ctypes.data_as(ct.c_void_p) if a is not None else None  # noqa: E731
+        self._lib_mod.check("usv_batch_sharded", self.lib.usv_batch_sharded(
+            self.handle, vp(L), vp(R), batch, self.H * self.W, self.W, vp(disp), vp(dist), vp(lut_arr),
+            int(bool(with_distance))))
+        return disp, dist
