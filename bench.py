@@ -11,6 +11,12 @@ disparity maps over RCCL (xGMI), overlapped with the next step's compute.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
 
+`--gpus N` must equal the launcher's WORLD_SIZE.  Without a launcher (no
+WORLD_SIZE in the environment) and N > 1, bench.py starts the N ranks itself
+(torch.distributed.run as a CHILD process, before anything touches the GPU)
+and exits with its status; fewer than N visible GPUs is an error.  It never
+reports a one-rank run for --gpus N > 1.
+
 Prints ONE JSON line on rank 0 (the driver's contract) with "roofline" for
 the dominant kernel (HBM algorithmic bytes / avg kernel time, HIP events on
 the kernel's stream) and, at N=1, "cpu_baseline" (the C oracle's
@@ -179,16 +185,67 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
     return res
 
 
+def spawn_ranks(n: int, need_gpus: bool) -> int:
+    """Run this script as N ranks under torch.distributed.run (a child process; this process has not
+    touched the GPU: torch.cuda.device_count() does not initialise it) and return its exit status."""
+    import socket
+    import subprocess
+    if need_gpus:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    with socket.socket() as sock:
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
+
+
+def plumbing_rehearsal(a, world: int, rank: int) -> None:
+    """USV_BENCH_PLUMBING=1: the N-rank launch contract on CPU (gloo), no GPU and no kernel -- rank
+    spawn, the barriers around the timed region, max-over-ranks timing and the rank-0 JSON line.
+    Its record carries value null: it measures nothing."""
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0, float(rank)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": BASELINE_METRIC, "value": None, "unit": "disparity-pixels/s", "n_gpus": world,
+                          "steps": a.steps, "warmup": a.warmup, "ms_per_step": None, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "plumbing rehearsal: no GPU, no kernel (USV_BENCH_PLUMBING=1)",
+                          "config": {"workload": "none", "parallelism": f"{world} gloo ranks"},
+                          "max_rank_seen": int(t[1])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    plumbing = os.environ.get("USV_BENCH_PLUMBING") == "1"
     # USV_BENCH_REHEARSE=1: several ranks on one GPU over gloo (a 1-GPU rehearsal of the N>1 code
     # path; use with --gather none, its numbers mean nothing)
     rehearse = os.environ.get("USV_BENCH_REHEARSE") == "1"
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus, need_gpus=not (plumbing or rehearse)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if plumbing:
+        plumbing_rehearsal(a, world, rank)
+        return
     if rehearse:
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
