@@ -21,6 +21,11 @@
  *   - ResolveMatchList P/Main.cpp:432-477 and IDMatcher P/Main.cpp:483-499,
  *     pinned by the SURVEY.md §8(c) golden vectors (duplicate-emitting
  *     conflict pass; comma-operator Point3i).
+ *   - GenerateMatchingList P/Main.cpp:403-426 with OpenCV 3.0 matchShapes /
+ *     moments / HuMoments / contourArea, and the centre points of
+ *     P/Main.cpp:1120-1143 with convexHull / minAreaRect / RotatedRect::points
+ *     (shape_oracle.c).  Restated from OpenCV 3.0.0's published algorithms;
+ *     parity vs OpenCV itself unpinned (absent, and the reference has no fixtures).
  *   - SURVEY.md §8(f) rows 1 and 3 (rectify_oracle.c, preproc_oracle.c):
  *     initUndistortRectifyMap + remap (P/Main.cpp:351-359), BGR2HSV /
  *     equalizeHist / HSV2BGR / BGR2GRAY (P/Main.cpp:365-371, 919-921), the
@@ -96,6 +101,24 @@ int usv_oracle_resolve_match_list(const usv_oracle_match* in, int n_in, usv_orac
 /* P/Main.cpp:483-499; out gets 3 ints per triple; returns the triple count. */
 int usv_oracle_id_matcher(const usv_oracle_match* cur, int n_cur,
                           const usv_oracle_match* old, int n_old, int* out_xyz);
+
+/* ---- A4 / A7: OpenCV 3.0 contour functions (shape_oracle.c; parity vs OpenCV unpinned) ---- */
+/* Contours are n int (x, y) points interleaved. */
+void usv_oracle_hu_moments(const int* pts, int n, double* hu7);
+double usv_oracle_match_shapes_i1(const int* pts_a, int n_a, const int* pts_b, int n_b);
+double usv_oracle_contour_area(const int* pts, int n); /* unoriented */
+/* P/Main.cpp:403-426; contour i of a set = pts[2*off[i] .. 2*off[i+1]); returns the count written. */
+int usv_oracle_generate_matching_list(const int* pts_a, const int* off_a, int n_a, const int* pts_b,
+                                      const int* off_b, int n_b, usv_oracle_match* out);
+/* convexHull(clockwise = true, returnPoints = true): hull_xy gets 2 ints per hull point; returns the count. */
+int usv_oracle_convex_hull_cw(const int* pts, int n, int* hull_xy);
+/* minAreaRect: out5 = {cx, cy, width, height, angle deg}; returns the hull size. */
+int usv_oracle_min_area_rect(const int* pts, int n, float* out5);
+/* RotatedRect::points of out5: 4 corners, 8 floats. */
+void usv_oracle_rect_points(const float* r5, float* pt8);
+/* P/Main.cpp:1120-1143: centre point per match (out_xy 2 floats each); returns the count. */
+int usv_oracle_match_centroids(const int* pts, const int* off, int n_contours, const usv_oracle_match* matches,
+                               int n_matches, float* out_xy);
 
 /* ---- §8(f) row 1: rectification (rectify_oracle.c) ---- */
 /* 3x3 inverse, cv::invert n == 3 path; returns 0 when singular. */

@@ -36,6 +36,15 @@ _SIGS = {
     "usv_oracle_resolve_match_list": (c_int, [POINTER(oracle_match), c_int, POINTER(oracle_match)]),
     "usv_oracle_id_matcher": (c_int, [POINTER(oracle_match), c_int, POINTER(oracle_match), c_int,
                                       POINTER(c_int)]),
+    "usv_oracle_hu_moments": (None, [c_void_p, c_int, c_void_p]),
+    "usv_oracle_match_shapes_i1": (c_double, [c_void_p, c_int, c_void_p, c_int]),
+    "usv_oracle_contour_area": (c_double, [c_void_p, c_int]),
+    "usv_oracle_generate_matching_list": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                                  POINTER(oracle_match)]),
+    "usv_oracle_convex_hull_cw": (c_int, [c_void_p, c_int, c_void_p]),
+    "usv_oracle_min_area_rect": (c_int, [c_void_p, c_int, c_void_p]),
+    "usv_oracle_rect_points": (None, [c_void_p, c_void_p]),
+    "usv_oracle_match_centroids": (c_int, [c_void_p, c_void_p, c_int, POINTER(oracle_match), c_int, c_void_p]),
     "usv_oracle_invert3": (c_int, [c_void_p, c_void_p]),
     "usv_oracle_rectify_params": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "usv_oracle_rectify_map": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
@@ -86,6 +95,74 @@ def oracle_sad(L, R, D, w, metric="sad", variant="sliding", threads=0):
 
 def _p(a):
     return a.ctypes.data
+
+
+def _pts(c):
+    import numpy as np
+    return np.ascontiguousarray(np.asarray(c, dtype=np.int32).reshape(-1)) if len(c) else np.zeros(2, np.int32)
+
+
+def _flat(contours):
+    import numpy as np
+    pts = [p for c in contours for p in c]
+    off = np.zeros(len(contours) + 1, dtype=np.int32)
+    off[1:] = np.cumsum([len(c) for c in contours])
+    flat = np.asarray(pts, dtype=np.int32).reshape(-1) if pts else np.zeros(2, dtype=np.int32)
+    return np.ascontiguousarray(flat), off
+
+
+def oracle_hu(c):
+    import numpy as np
+    out = np.zeros(7)
+    pc = _pts(c)  # keep the array alive across the call
+    load_oracle().usv_oracle_hu_moments(_p(pc), len(c), _p(out))
+    return out
+
+
+def oracle_match_shapes_i1(a, b):
+    pa, pb = _pts(a), _pts(b)
+    return load_oracle().usv_oracle_match_shapes_i1(_p(pa), len(a), _p(pb), len(b))
+
+
+def oracle_contour_area(c):
+    pc = _pts(c)
+    return load_oracle().usv_oracle_contour_area(_p(pc), len(c))
+
+
+def oracle_generate_matching_list(A, B):
+    pa, oa = _flat(A)
+    pb, ob = _flat(B)
+    out = (oracle_match * max(len(A) * len(B), 1))()
+    n = load_oracle().usv_oracle_generate_matching_list(_p(pa), _p(oa), len(A), _p(pb), _p(ob), len(B), out)
+    return [(out[i].left, out[i].right, out[i].value) for i in range(n)]
+
+
+def oracle_convex_hull(c):
+    import numpy as np
+    out = np.zeros(2 * max(len(c), 1), np.int32)
+    pc = _pts(c)
+    n = load_oracle().usv_oracle_convex_hull_cw(_p(pc), len(c), _p(out))
+    return [tuple(int(v) for v in out[2 * i:2 * i + 2]) for i in range(n)]
+
+
+def oracle_min_area_rect(c):
+    """-> ((cx, cy), (w, h), angle) float32 values, as host.min_area_rect."""
+    import numpy as np
+    out = np.zeros(5, np.float32)
+    pc = _pts(c)
+    load_oracle().usv_oracle_min_area_rect(_p(pc), len(c), _p(out))
+    return (out[0], out[1]), (out[2], out[3]), out[4]
+
+
+def oracle_match_centroids(contours, matches):
+    import numpy as np
+    p, off = _flat(contours)
+    arr = (oracle_match * max(len(matches), 1))()
+    for i, (l, r, v) in enumerate(matches):
+        arr[i].left, arr[i].right, arr[i].value = l, r, v
+    out = np.zeros(2 * max(len(matches), 1), np.float32)
+    n = load_oracle().usv_oracle_match_centroids(_p(p), _p(off), len(contours), arr, len(matches), _p(out))
+    return [(out[2 * i], out[2 * i + 1]) for i in range(n)]
 
 
 def oracle_rectify_params(K, dist, R, P):
