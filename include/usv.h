@@ -39,6 +39,8 @@
  *   usv_rectify_params / _map initUndistortRectifyMap(..., CV_16SC2, ...),
  *                             P/Main.cpp:352,357 (the
  *                             reference rebuilds it every frame, we build once)
+ *   usv_load_calibration,     LoadCalibrationData, P/Main.cpp:329-349 (FileStorage
+ *   usv_calibration_rectify_params  XML read without OpenCV)
  *   usv_remap_linear_u8,      remap(INTER_LINEAR, BORDER_CONSTANT, Scalar()),
  *   usv_rectify_pair_u8       P/Main.cpp:353,358 (one launch for both cameras)
  *   usv_bgr2hsv_hist_u8,      cvtColor BGR2HSV P/Main.cpp:919 + LightingCorrection
@@ -304,6 +306,31 @@ usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW,
                                int cn, const int16_t* map1L, const uint16_t* map2L,
                                const int16_t* map1R, const uint16_t* map2R, int W, int H,
                                uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
+
+/* ---- calibration file: LoadCalibrationData, P/Main.cpp:329-349 ---- */
+
+/* A small dense matrix, row-major doubles (rows = cols = 0: empty, as an unread cv::Mat). */
+typedef struct {
+    int rows, cols;
+    double data[16];
+} usv_mat;
+
+/* CalibrationDataParameters (P/Main.cpp:175-180) without the maps, the reference's spellings. */
+typedef struct {
+    usv_mat intrinsicL, distCoeffsL, intrinsicR, distCoeffsR;
+    usv_mat RotationMat, TranslationMat, EssentailMat, FundamentalMat;
+    usv_mat RectificationTransformMatL, RectificationTransformMatR, ProjectionMatL, ProjectionMatR,
+        Disparity2DepthMappingMat;
+} usv_calibration;
+
+/* HOST: read the 13 matrices of an OpenCV FileStorage XML file (opencv_storage
+ * root, type_id="opencv-matrix" nodes); absent names stay empty.  At most 16
+ * elements per matrix (USV_ERR_UNSUPPORTED otherwise). */
+usv_status usv_load_calibration(const char* path, usv_calibration* out);
+
+/* HOST: usv_rectify_params from one camera's four matrices (left != 0: the L
+ * set), the arguments of initUndistortRectifyMap at P/Main.cpp:352 / 357. */
+usv_status usv_calibration_rectify_params(const usv_calibration* cal, int left, double* params);
 
 /* ---- per-frame colour chain and masks, all DEVICE ---- */
 

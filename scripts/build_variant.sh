@@ -12,6 +12,6 @@ mkdir -p build_variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -ffp-contract=off "$@" \
     -c $C/$SRC.hip -o build_variants/$name.var.o
 objs=$(ls $C/build/*.o | grep -v "/$SRC.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.var.o $objs
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.var.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f build_variants/$name.var.o
 echo built build_variants/$name.so

@@ -41,6 +41,21 @@ class UsvError(RuntimeError):
         self.status = status
 
 
+class usv_mat(ctypes.Structure):
+    _fields_ = [("rows", c_int), ("cols", c_int), ("data", c_double * 16)]
+
+
+CALIBRATION_NAMES = ["intrinsicL", "distCoeffsL", "intrinsicR", "distCoeffsR", "RotationMat", "TranslationMat",
+                     "EssentailMat", "FundamentalMat", "RectificationTransformMatL", "RectificationTransformMatR",
+                     "ProjectionMatL", "ProjectionMatR", "Disparity2DepthMappingMat"]
+
+
+class usv_calibration(ctypes.Structure):
+    """CalibrationDataParameters (P/Main.cpp:175-180) in include/usv.h's layout."""
+
+    _fields_ = [(n, usv_mat) for n in CALIBRATION_NAMES]
+
+
 class usv_match(ctypes.Structure):
     """Layout of P/Match.hpp:4-12 (unsigned, unsigned, double)."""
 
@@ -102,6 +117,8 @@ SIGNATURES = {
     "usv_frame_prep_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                   c_int, c_void_p, c_int, c_void_p]),
     "usv_motion_mask_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "usv_load_calibration": (c_int, [c_char_p, POINTER(usv_calibration)]),
+    "usv_calibration_rectify_params": (c_int, [POINTER(usv_calibration), c_int, c_void_p]),
     "usv_colour_mask_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_int, c_void_p]),
 }
