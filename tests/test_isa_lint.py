@@ -86,8 +86,9 @@ def test_few_full_vmem_drains(fast_kernels):
 def test_split_scalar_loads_do_not_clobber_their_base(fast_kernels):
     for name, ins in fast_kernels.items():
         for a, b in zip(ins, ins[1:]):
-            m1 = re.match(r"s_load_dwordx4 (\S+), (\S+), 0x0$", a)
-            m2 = re.match(r"s_load_dword(?:x2)? (\S+), (\S+), 0x10$", b)
+            # immediate-offset form (warm-up rows) and SGPR-offset form (steady rows)
+            m1 = re.match(r"s_load_dwordx4 (\S+), (\S+), (?:0x0|s\d+)$", a)
+            m2 = re.match(r"s_load_dword(?:x2)? (\S+), (\S+), (?:0x10|s\d+ offset:0x10)$", b)
             if m1 and m2 and m1.group(2) == m2.group(2):
                 assert not (_sregs(m1.group(1)) & _sregs(m2.group(2))), (name, a, b)
 
@@ -132,7 +133,7 @@ def inflight_scalar_load_hazards(ins):
         if i.startswith("s_waitcnt") and "lgkmcnt(0)" in i:
             cur = set()
         elif i.startswith("s_load"):
-            if _sregs(toks[2]) & cur:
+            if any(_sregs(t) & cur for t in toks[2:]):
                 bad.add((k, str(i)))
             cur |= _sregs(toks[1])
         elif any(_sregs(t) & cur for t in toks[1:]):
@@ -154,5 +155,5 @@ def test_lds_dma_m0_wait_state(fast_kernels):
     # GFX9: an SALU write of M0 needs one wait state before an LDS-DMA reads it
     for name, ins in fast_kernels.items():
         for a, b in zip(ins, ins[1:]):
-            if b.startswith("global_load_lds"):
+            if b.startswith("global_load_lds") or (b.startswith("buffer_load") and b.endswith(" lds")):
                 assert not re.match(r"s_\w+ m0,", a), (name, a, b)

@@ -417,6 +417,60 @@ __device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uin
     }
 }
 
+// Steady-state row addressing without 64-bit pointer arithmetic: the R row's LDS-DMAs
+// are MUBUF loads whose soffset carries the row offset (buffer over R - kDmaBias,
+// no range limit), the L row segment an s_load with an SGPR offset; both offsets are
+// running sums clamped at the last image row (two SALU per pointer and row instead of
+// clamp, multiply and a 64-bit add).  Warm-up rows keep the clamped per-row form.
+#ifndef USV_RUN_ADDR
+#define USV_RUN_ADDR 1
+#endif
+template <int NQ>
+__device__ __forceinline__ void dma_row_buf(su4 rsrc, uint32_t soff, const uint32_t (&vo)[NQ], uint32_t m0) {
+    static_assert(NQ >= 1 && NQ <= 5, "1..5 DMAs per row");
+    if constexpr (NQ == 1)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_ubyte %0, %2, %3 offen lds"
+                     :: "v"(vo[0]), "s"(m0), "s"(rsrc), "s"(soff) : "memory", "m0");
+    else if constexpr (NQ == 2)
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_ubyte %0, %3, %4 offen lds\n\t"
+                     "buffer_load_ubyte %1, %3, %4 offen offset:256 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "s"(m0), "s"(rsrc), "s"(soff) : "memory", "m0");
+    else if constexpr (NQ == 3)
+        asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_ubyte %0, %4, %5 offen lds\n\t"
+                     "buffer_load_ubyte %1, %4, %5 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %4, %5 offen offset:512 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(m0), "s"(rsrc), "s"(soff) : "memory", "m0");
+    else if constexpr (NQ == 4)
+        asm volatile("s_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_ubyte %0, %5, %6 offen lds\n\t"
+                     "buffer_load_ubyte %1, %5, %6 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %5, %6 offen offset:512 lds\n\t"
+                     "buffer_load_ubyte %3, %5, %6 offen offset:768 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(m0), "s"(rsrc), "s"(soff)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %5\n\ts_nop 0\n\tbuffer_load_ubyte %0, %6, %7 offen lds\n\t"
+                     "buffer_load_ubyte %1, %6, %7 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %6, %7 offen offset:512 lds\n\t"
+                     "buffer_load_ubyte %3, %6, %7 offen offset:768 lds\n\t"
+                     "buffer_load_ubyte %4, %6, %7 offen offset:1024 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "s"(m0), "s"(rsrc), "s"(soff)
+                     : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ typename SWords<N>::T s_load_words_off(const uint8_t* p, uint32_t off) {
+    typename SWords<N>::T w;
+    if constexpr (N == 8) {
+        asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(w) : "s"(p), "s"(off) : "memory");
+    } else if constexpr (N == 6) {
+        asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dwordx2 %1, %2, %3 offset:0x10"
+                     : "=&s"(w.a), "=&s"(w.b) : "s"(p), "s"(off) : "memory");
+    } else {
+        asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dword %1, %2, %3 offset:0x10"
+                     : "=&s"(w.a), "=&s"(w.b) : "s"(p), "s"(off) : "memory");
+    }
+    return w;
+}
+
 #if USV_STAMPS
 // phases: 0 DMA wait, 1 L-word wait, 2 chain+H+S, 3 keys+reduce, 4 flush, 5 rows, 6 waves, 7 total
 __device__ unsigned long long g_usv_stamps[8];
@@ -506,6 +560,20 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     };
     const uint8_t* const Lseg = L + LS::base(x0);
     const uint8_t* const Rdma = (USV_DMA_ONE_M0 && !C::STATIC_RING) ? R - kDmaBias : R;
+    constexpr bool RUN = USV_RUN_ADDR && USV_DMA_ONE_M0 && !C::STATIC_RING;
+    // raw (unclamped) byte offsets of the rows the next steady row loads: L row t + 1, R row t + PD
+    const int y0 = y_begin - RAD;
+    const int last_off = Hm1 * a.pitch;
+    int rawL = (y0 + WIN + 1) * a.pitch, rawR = (y0 + WIN + PD) * a.pitch;
+    const su4 rsrc = [&] {
+        const uint64_t base = reinterpret_cast<uint64_t>(Rdma);
+        su4 r;
+        r[0] = (uint32_t)base;
+        r[1] = (uint32_t)(base >> 32);  // stride 0: raw buffer
+        r[2] = 0xFFFFFFFFu;             // num_records: no range limit (offsets stay inside R)
+        r[3] = 0x00020000u;             // gfx9 raw-buffer word 3 (CK_BUFFER_RESOURCE_3RD_DWORD)
+        return r;
+    }();
 
     // ---- R rows: LDS-DMA into the ring, PD rows ahead ----
     // Rows past the band are clamped to real rows: harmless extra loads.
@@ -561,10 +629,18 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         wait_vmcnt<(PD - 1) * NDMA>();  // row t has landed in LDS
         __builtin_amdgcn_wave_barrier();
         if constexpr (USV_PRIO == 3) set_prio((prio_slot + t) % 3);
-        if constexpr (C::STATIC_RING)
+        if constexpr (C::STATIC_RING) {
             issue_dma(t + PD, std::integral_constant<int, (I + PD) % NB>{});
-        else
+        } else if constexpr (RUN && !WARM) {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));  // opaque: one row's offset at a time
+            const int buf = (t + PD) & (NB - 1);
+            if (USV_EXP != 1)
+                dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            rawR = rr + a.pitch;
+        } else {
             issue_dma(t + PD, std::integral_constant<int, -1>{});
+        }
         USV_STAMP(0);
 
         uint32_t Lv[C::NPOS];
@@ -646,7 +722,14 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #if USV_STAMPS
         st.rows++;
 #endif
-        load_lw(t + 1);
+        if constexpr (RUN && !WARM) {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_off<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        } else {
+            load_lw(t + 1);
+        }
         // Keep rows apart: interleaving the unrolled rows only raises
         // register pressure (spills whose reloads would drain the DMA queue).
         __builtin_amdgcn_sched_barrier(0);
