@@ -124,9 +124,9 @@ struct Cfg {
 //              may overlap its neighbour; both write identical values):
 //              load up to column W-1, the last r positions replicate it.
 enum : int { kInterior = 0, kLeft = 1, kRight = 2 };
-template <int RAD, int EDGE>
+template <int RAD, int EDGE, int KK = kK>
 struct LSeg {
-    static constexpr int K = kK, NPOS = K + 2 * RAD;
+    static constexpr int K = KK, NPOS = K + 2 * RAD;
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - r) mod 4 for x0 % 4 == 0
     static constexpr int NLD = EDGE == kInterior ? (LOFF + NPOS + 3) / 4
                              : EDGE == kLeft     ? (K + RAD + 3) / 4
@@ -138,7 +138,7 @@ struct LSeg {
                                  : (LOFF + j < LOFF + K + RAD - 1 ? LOFF + j : LOFF + K + RAD - 1);
     }
     static_assert(EDGE != kRight || (LOFF + K + RAD) % 4 == 0, "right segment ends on a dword");
-    static_assert(NLD == 5 || NLD == 6 || NLD == 8, "scalar segment is 5, 6 or 8 dwords");
+    static_assert(NLD == 4 || NLD == 5 || NLD == 6 || NLD == 8, "scalar segment is 4, 5, 6 or 8 dwords");
 };
 
 // An L byte that sits at byte 0 of its dword is used as the whole dword: the
@@ -378,6 +378,7 @@ using su4 = uint32_t __attribute__((ext_vector_type(4)));
 using su2 = uint32_t __attribute__((ext_vector_type(2)));
 using su8 = uint32_t __attribute__((ext_vector_type(8)));
 template <int N> struct SWords;
+template <> struct SWords<4> { using T = su4; };
 template <> struct SWords<5> { struct T { su4 a; uint32_t b; }; };
 template <> struct SWords<6> { struct T { su4 a; su2 b; }; };
 template <> struct SWords<8> { using T = su8; };
@@ -386,6 +387,8 @@ __device__ __forceinline__ typename SWords<N>::T s_load_words(const uint8_t* p) 
     typename SWords<N>::T w;
     if constexpr (N == 8) {
         asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(w) : "s"(p) : "memory");
+    } else if constexpr (N == 4) {
+        asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(w) : "s"(p) : "memory");
     } else if constexpr (N == 6) {
         asm volatile("s_load_dwordx4 %0, %2, 0x0\n\ts_load_dwordx2 %1, %2, 0x10"
                      : "=&s"(w.a), "=&s"(w.b) : "s"(p) : "memory");
@@ -399,7 +402,7 @@ __device__ __forceinline__ typename SWords<N>::T s_load_words(const uint8_t* p) 
 // are in/out operands so nothing that reads them can be scheduled above.
 template <int N>
 __device__ __forceinline__ void wait_lgkm0(typename SWords<N>::T& w) {
-    if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w) : : "memory");
+    if constexpr (N == 8 || N == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w) : : "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w.a), "+s"(w.b) : : "memory");
 }
 template <int N>
@@ -409,6 +412,9 @@ __device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uin
     if constexpr (N == 8) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = w[i];
+    } else if constexpr (N == 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = w[i];
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = w.a[i];
@@ -461,6 +467,8 @@ __device__ __forceinline__ typename SWords<N>::T s_load_words_off(const uint8_t*
     typename SWords<N>::T w;
     if constexpr (N == 8) {
         asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(w) : "s"(p), "s"(off) : "memory");
+    } else if constexpr (N == 4) {
+        asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(w) : "s"(p), "s"(off) : "memory");
     } else if constexpr (N == 6) {
         asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dwordx2 %1, %2, %3 offset:0x10"
                      : "=&s"(w.a), "=&s"(w.b) : "s"(p), "s"(off) : "memory");
@@ -1035,6 +1043,370 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ===================================================================================
+// Paired-disparity kernel (D > 64, even D, 5 <= r <= 7): lane = two ADJACENT disparities.
+//
+// Lane l of wave w owns d = 2 (NW l + w) in the low half of its packed-u16 sums and
+// d + 1 in the high half, for K = 8 output columns.  The two share the L byte of each
+// chain step (one SGPR for both v_sad_u8 and v_sad_hi_u8) and their R bytes are adjacent
+// columns of the staged row: step j reads entries j (d + 1) and j + 1 (d), so a lane reads
+// K + 2r + 1 staged entries for 2 x K (column, disparity) pairs per step instead of
+// K + 2r for K, and a whole 128-disparity search is ONE wave: per (pixel, disparity) half
+// the L-byte extraction, row addressing and LDS-DMA instructions of the column-paired
+// kernel above, ~30 % less LDS traffic, and no cross-wave combine barrier at D <= 128.
+// Keys: lo = (cost << 8) | d, hi = (cost << 8) | (d + 1); the transpose gives lane
+// 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
+// rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
+// ===================================================================================
+template <int RAD, int NW>
+struct PCfg {
+    static constexpr int K = 8;
+    static constexpr int WIN = 2 * RAD + 1;
+    static constexpr int NPOS = K + 2 * RAD;            // chain steps
+    static constexpr int NE = NPOS + 1;                 // staged entries a lane reads per row
+    static constexpr int VEC = NW >= 2 ? 4 : 2;         // lane offsets are 2 NW entries apart
+    static constexpr int NE_V = (NE + VEC - 1) / VEC * VEC;
+    static constexpr int NR = 2 * NW * 63 + NE_V;       // entries a wave stages per row
+    static constexpr int NQ = (NR + 63) / 64;           // DMA instructions per row
+    static constexpr int NRS = NQ * 64;
+    static constexpr int NB = NW == 1 ? 8 : 4;          // ring slots per wave
+    static constexpr int PD = NB - 1;
+    static constexpr int KRB = WIN;
+    static constexpr int RBUF_OFF = 0;
+    static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
+    static constexpr int TB_WORDS = K * 64;
+    static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
+    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
+    static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
+    static_assert(RAD >= 5 && RAD <= 7, "paired kernel: 11 <= w <= 15");
+    static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
+    static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
+};
+
+template <int RAD, int NW, int EDGE>
+__device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                               uint8_t* __restrict__ disp, double* __restrict__ dist,
+                                               const MatchArgs& a, uint32_t* smem, int lane, int wave, int x0,
+                                               int y_begin, int y_end) {
+    using C = PCfg<RAD, NW>;
+    using LS = LSeg<RAD, EDGE, C::K>;
+    using LWords = typename SWords<LS::NLD>::T;
+    constexpr int WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
+    constexpr int NDMA = C::NQ;
+    // lane l owns (d, d + 1), d = 2 (NW l + wave); lanes past the last full pair replay it
+    const int lmax = (a.D / 2 - 1 - wave) / NW;
+    const int l_eff = min(lane, lmax);
+    const int cbase = x0 - RAD - (2 * (NW * 63 + wave) + 1);  // first R column this wave stages
+    uint32_t* rbuf = smem + C::RBUF_OFF + wave * NB * C::NRS;
+    uint32_t* comb = smem + C::COMB_OFF;
+    uint32_t* tb = smem + C::TB_OFF + wave * C::TB_WORDS;
+    // transposed reads: lane m = 8p + q takes words 64 p + 8 q .. + 7 as two 16-B windows,
+    // lanes q >= 4 the second first (an 8-lane phase then covers 32 distinct banks)
+    uint32_t rdw[2], dlo[2], dhi[2];
+    {
+        const int p = lane >> 3, q = lane & 7, rot = (q >> 2) & 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int win = j ^ rot;
+            rdw[j] = (uint32_t)(16 * p + 2 * q + win);  // uint4 index: (64 p + 8 q + 4 win) / 4
+            uint32_t lo = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int src = 8 * q + 4 * win + e;
+                lo |= (uint32_t)(2 * (NW * min(src, lmax) + wave)) << (8 * e);
+            }
+            dlo[j] = lo;
+            dhi[j] = lo + 0x01010101u;  // d even: + 1 per byte, no carry
+        }
+    }
+    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
+    const int s_l = 2 * NW * (63 - l_eff);  // this lane's first staged entry
+    const int nout = y_end - y_begin;
+    const int T = nout + 2 * RAD;
+    const int Hm1 = a.H - 1, Wm1 = a.W - 1;
+    auto row_off = [&](int t) -> uint32_t {
+        const int y = min(max(y_begin - RAD + t, 0), Hm1);
+        return (uint32_t)(y * a.pitch);
+    };
+    const uint8_t* const Lseg = L + LS::base(x0);
+    const uint8_t* const Rdma = R - kDmaBias;
+    const int y0 = y_begin - RAD;
+    const int last_off = Hm1 * a.pitch;
+    int rawL = (y0 + WIN + 1) * a.pitch, rawR = (y0 + WIN + PD) * a.pitch;
+    const su4 rsrc = [&] {
+        const uint64_t base = reinterpret_cast<uint64_t>(Rdma);
+        su4 r;
+        r[0] = (uint32_t)base;
+        r[1] = (uint32_t)(base >> 32);
+        r[2] = 0xFFFFFFFFu;
+        r[3] = 0x00020000u;
+        return r;
+    }();
+    uint32_t colRb[C::NQ];
+#pragma unroll
+    for (int i = 0; i < C::NQ; ++i)
+        colRb[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1) + kDmaBias - 256u * (uint32_t)i;
+    const uint32_t rbase = lds_addr(rbuf);
+    auto issue_dma = [&](int t) {
+        const int buf = t & (NB - 1);
+        dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+    };
+    LWords lw_next;
+    auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(Lseg + row_off(t)); };
+
+    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
+        constexpr bool WARM = decltype(warm_tag)::value;
+        constexpr int I = decltype(i_tag)::value;
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        wait_vmcnt<(PD - 1) * NDMA>();
+        __builtin_amdgcn_wave_barrier();
+        if constexpr (WARM) {
+            issue_dma(t + PD);
+        } else {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));
+            const int buf = (t + PD) & (NB - 1);
+            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            rawR = rr + a.pitch;
+        }
+        uint32_t Lv[NPOS];
+        {
+            LWords cur = lw_next;
+            wait_lgkm0<LS::NLD>(cur);
+            uint32_t lw[8];
+            unpack_words<LS::NLD>(cur, lw);
+#pragma unroll
+            for (int j = 0; j < NPOS; ++j) {
+                const int bidx = LS::byte(j);
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+                else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+            }
+        }
+        using VT = typename VecT<C::VEC>::T;
+        int boff = (t & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
+        uint32_t E[C::NE_V];
+#pragma unroll
+        for (int k = 0; k < C::NE_V / C::VEC; ++k) {
+            const VT v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+        // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half)
+        uint32_t A[NPOS + 1];
+        A[0] = 0;
+#pragma unroll
+        for (int j = 0; j < NPOS; ++j)
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+#pragma unroll
+        for (int x = 0; x < K; ++x) {
+            const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
+            if constexpr (WARM) S[x] = S[x] + h;
+            else S[x] = (S[x] - ring[I][x]) + h;
+            ring[I][x] = h;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (WARM) {
+            load_lw(t + 1);
+        } else {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_off<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    int cb = 0, y_chunk = y_begin;
+    auto flush = [&](int rows) {
+        if constexpr (NW > 1) lds_barrier();
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int items = rows * K;
+        for (int i = tid; i < items; i += NW * 64) {
+            const int row = i / K, p = i - row * K;
+            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
+            const uint32_t dv = key & 0xFFu;
+            const size_t y = (size_t)(y_chunk + row);
+            disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
+            if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
+        }
+        y_chunk += rows;
+        cb ^= 1;
+    };
+    auto emit = [&](const uint32_t(&S)[K], int slot) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        asm volatile("" ::: "memory");
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint4 q = reinterpret_cast<const uint4*>(tb)[rdw[j]];
+            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[8 * j + 2 * e] = __builtin_amdgcn_perm(w4[e], dlo[j], 0x0c050400u + (uint32_t)e);
+                v[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w4[e], dhi[j], 0x0c070600u + (uint32_t)e);
+            }
+        }
+        asm volatile("" ::: "memory");
+        uint32_t b0 = min(min(v[0], v[1]), v[2]), b1 = min(min(v[3], v[4]), v[5]);
+        uint32_t b2 = min(min(v[6], v[7]), v[8]), b3 = min(min(v[9], v[10]), v[11]);
+        uint32_t b4 = min(min(v[12], v[13]), v[14]);
+        b0 = min(min(b0, b1), b2);
+        b3 = min(min(b3, b4), v[15]);
+        uint32_t m = min(b0, b3);
+        m = min(m, dpp<kQuadSwap1>(m));
+        m = min(m, dpp<kQuadSwap2>(m));
+        m = min(m, dpp<kRowHalfMirror>(m));
+        comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 3)] = m;
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    uint32_t S[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) S[i] = 0;
+    uint32_t ring[WIN][K];
+    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
+    load_lw(0);
+    using WarmT = std::integral_constant<bool, true>;
+    using SteadyT = std::integral_constant<bool, false>;
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
+    }(std::make_integer_sequence<int, WIN>{});
+    emit(S, 0);
+    auto step = [&](int t0, auto i_tag) {
+        constexpr int I = decltype(i_tag)::value;
+        do_row(t0 + I, SteadyT{}, i_tag, S, ring);
+        emit(S, (I + 1) % WIN);
+        if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+    };
+    for (int t0 = WIN; t0 < T; t0 += WIN) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            bool go = true;
+            ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
+        }(std::make_integer_sequence<int, WIN>{});
+    }
+    wait_lgkm0<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
+    const int rest = nout % KRB;
+    if (rest) flush(rest);
+    wait_vmcnt<0>();
+}
+
+constexpr int pair_occ(int rad, int) { return rad >= 7 ? 2 : 3; }
+
+template <int RAD, int NW>
+__global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
+                                                              const uint8_t* __restrict__ R,
+                                                              uint8_t* __restrict__ disp,
+                                                              double* __restrict__ dist, MatchArgs a, BandPlan P) {
+    using C = PCfg<RAD, NW>;
+    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the work map of sad_fast_kernel (XCD-contiguous tile runs, generation-weighted bands)
+    const unsigned total = gridDim.x, lin = blockIdx.x;
+    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
+    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
+    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
+    const bool past = tile >= per_pair && P.extra > 0;
+    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
+    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
+    const unsigned pair = past ? 0u : tile / per_pair;
+    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
+    const unsigned long_run = base + 1u, split = rem * long_run;
+    auto gen_weight = [&](unsigned sb) -> unsigned {
+        const unsigned t = pair * per_pair + sb * nxt + col_xt;
+        const unsigned j = t < split ? t % long_run : (t - split) % base;
+        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
+        return (P.weights >> (8 * g)) & 0xFFu;
+    };
+    unsigned pre = 0, tot = 0;
+    for (unsigned sb = 0; sb < m_col; ++sb) {
+        const unsigned wgt = gen_weight(sb);
+        pre += sb < s ? wgt : 0u;
+        tot += wgt;
+    }
+    const int xt = (int)col_xt;
+    const int n_xt = P.n_xt;
+    int x0 = xt * C::K;
+    if (xt == n_xt - 1) x0 = a.W - C::K;
+    else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
+    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
+    L += (size_t)pair * a.pair_stride;
+    R += (size_t)pair * a.pair_stride;
+    disp += (size_t)pair * a.disp_stride;
+    if (dist) {
+        dist += (size_t)pair * a.dist_stride;
+        double* lut_s = reinterpret_cast<double*>(smem + C::LUT_OFF);
+        for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
+    }
+    __syncthreads();
+    if (y_end <= y_begin) return;
+    if (xt == 0)
+        pair_band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    else if (xt == n_xt - 1)
+        pair_band_loop<RAD, NW, kRight>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    else
+        pair_band_loop<RAD, NW, kInterior>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+}
+
+template <int RAD, int NW>
+int resident_pair_blocks_per_cu() {
+    static const int n = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair_kernel<RAD, NW>, NW * 64, 0) != hipSuccess ||
+            v <= 0)
+            v = 1;
+        return v;
+    }();
+    return n;
+}
+
+template <int RAD, int NW>
+hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
+    constexpr int K = PCfg<RAD, NW>::K, WIN = 2 * RAD + 1;
+    BandPlan P{};
+    P.n_xt = (a.W + K - 1) / K;
+    const int per_cu = resident_pair_blocks_per_cu<RAD, NW>();
+    const long slots = (long)cu_count() * per_cu;
+    const long NC = (long)P.n_xt * a.batch;
+    long m = slots / NC;
+    if (m < 1) m = 1;
+    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    if (m > m_max) m = m_max;
+    P.m = (int)m;
+    const long ex = slots - NC * m;
+    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    const long total = NC * m + P.extra;
+    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
+    if (P.gen_g < 1) P.gen_g = 1;
+    const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
+    P.weights = three ? USV_GEN_WEIGHTS : 0x01010101u;
+    dim3 grid((unsigned)total), block(NW * 64);
+    hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
+    return hipGetLastError();
+}
+
+#ifndef USV_PAIR
+#define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
+#endif
+bool pair_path_supported(const MatchArgs& a) {
+    return USV_PAIR && a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15;
+}
+template <int RAD>
+hipError_t launch_pair_r(const MatchArgs& a, hipStream_t s) {
+    return a.D <= 128 ? launch_pair_rn<RAD, 1>(a, s) : launch_pair_rn<RAD, 2>(a, s);
+}
+
 template <int RAD>
 hipError_t launch_r(const MatchArgs& a, hipStream_t s) {
     if (a.D <= 64) return launch_rn<RAD, 1>(a, s);
@@ -1074,6 +1446,14 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
 #ifdef USV_DEV_ONLY_RAD  // development: build a single instantiation for ISA inspection
     return launch_rn<USV_DEV_ONLY_RAD, USV_DEV_ONLY_NW>(a, s);
 #else
+    if (pair_path_supported(a)) {
+        switch ((a.w - 1) / 2) {
+            case 5: return launch_pair_r<5>(a, s);
+            case 6: return launch_pair_r<6>(a, s);
+            case 7: return launch_pair_r<7>(a, s);
+            default: break;
+        }
+    }
     switch ((a.w - 1) / 2) {
         case 1: return launch_r<1>(a, s);
         case 2: return launch_r<2>(a, s);
