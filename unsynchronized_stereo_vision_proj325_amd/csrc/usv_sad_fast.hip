@@ -1369,6 +1369,13 @@ int resident_pair_blocks_per_cu() {
     return n;
 }
 
+// Generation weights of the paired kernel (one-wave workgroups, three generations per SIMD):
+// interleaved A/B on config C, 100:90:70 / 100:80:58 / 100:85:55 / 100:80:50 / 100:75:50 /
+// 100:70:45 = 69.75 / 68.61 / 67.63 / 67.42 / 67.27 / 68.25 us (profiles/probes_r02/ab_pair_weights_*).
+#ifndef USV_PAIR_GEN_WEIGHTS
+#define USV_PAIR_GEN_WEIGHTS 0x32324B64u  // 100, 75, 50, 50
+#endif
+
 template <int RAD, int NW>
 hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     constexpr int K = PCfg<RAD, NW>::K, WIN = 2 * RAD + 1;
@@ -1390,7 +1397,7 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
     const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
-    P.weights = three ? USV_GEN_WEIGHTS : 0x01010101u;
+    P.weights = three ? USV_PAIR_GEN_WEIGHTS : 0x01010101u;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
