@@ -1046,8 +1046,8 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 // ===================================================================================
 // Paired-disparity kernel (D > 64, even D, 5 <= r <= 7): lane = two ADJACENT disparities.
 //
-// Lane l of wave w owns d = 2 (NW l + w) in the low half of its packed-u16 sums and
-// d + 1 in the high half, for K = 8 output columns.  The two share the L byte of each
+// Lane l of wave w owns d = 2 (64 w + l) in the low half of its packed-u16 sums and
+// d + 1 in the high half, for K = 8 output columns (wave w: disparities [128 w, 128 w + 128)).  The two share the L byte of each
 // chain step (one SGPR for both v_sad_u8 and v_sad_hi_u8) and their R bytes are adjacent
 // columns of the staged row: step j reads entries j (d + 1) and j + 1 (d), so a lane reads
 // K + 2r + 1 staged entries for 2 x K (column, disparity) pairs per step instead of
@@ -1064,12 +1064,16 @@ struct PCfg {
     static constexpr int WIN = 2 * RAD + 1;
     static constexpr int NPOS = K + 2 * RAD;            // chain steps
     static constexpr int NE = NPOS + 1;                 // staged entries a lane reads per row
-    static constexpr int VEC = NW >= 2 ? 4 : 2;         // lane offsets are 2 NW entries apart
+    static constexpr int VEC = 2;                       // lane offsets are 2 entries apart
     static constexpr int NE_V = (NE + VEC - 1) / VEC * VEC;
-    static constexpr int NR = 2 * NW * 63 + NE_V;       // entries a wave stages per row
+    static constexpr int NR = 2 * 63 + NE_V;            // entries a wave stages per row
     static constexpr int NQ = (NR + 63) / 64;           // DMA instructions per row
     static constexpr int NRS = NQ * 64;
-    static constexpr int NB = NW == 1 ? 8 : 4;          // ring slots per wave
+    static constexpr int NB = 8;                        // ring slots per wave
+#ifndef USV_PAIR_SPLIT_R
+#define USV_PAIR_SPLIT_R 7  // radius from which the row's entries are read in two batches
+#endif
+    static constexpr int SPLIT = RAD >= USV_PAIR_SPLIT_R ? 2 : 1;
     static constexpr int PD = NB - 1;
     static constexpr int KRB = WIN;
     static constexpr int RBUF_OFF = 0;
@@ -1093,10 +1097,11 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     using LWords = typename SWords<LS::NLD>::T;
     constexpr int WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
     constexpr int NDMA = C::NQ;
-    // lane l owns (d, d + 1), d = 2 (NW l + wave); lanes past the last full pair replay it
-    const int lmax = (a.D / 2 - 1 - wave) / NW;
+    // lane l owns (d, d + 1), d = 2 (64 wave + l); lanes past the last full pair replay it
+    const int lmax = min(63, a.D / 2 - 1 - 64 * wave);
     const int l_eff = min(lane, lmax);
-    const int cbase = x0 - RAD - (2 * (NW * 63 + wave) + 1);  // first R column this wave stages
+    const int dwave = 128 * wave;
+    const int cbase = x0 - RAD - (dwave + 2 * 63 + 1);  // first R column this wave stages
     uint32_t* rbuf = smem + C::RBUF_OFF + wave * NB * C::NRS;
     uint32_t* comb = smem + C::COMB_OFF;
     uint32_t* tb = smem + C::TB_OFF + wave * C::TB_WORDS;
@@ -1112,18 +1117,20 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         for (int j = 0; j < 2; ++j) {
             const int win = j ^ rot;
             rdw[j] = (uint32_t)(16 * p + 2 * q + win);  // uint4 index: (64 p + 8 q + 4 win) / 4
+            // source lanes past lmax replay lane lmax's data: the same cost with a larger d, so
+            // their keys never win and their d bytes need no clamp (max 2 (64 + 63) + 1 = 255)
             uint32_t lo = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int src = 8 * q + 4 * win + e;
-                lo |= (uint32_t)(2 * (NW * min(src, lmax) + wave)) << (8 * e);
+                lo |= (uint32_t)(dwave + 2 * src) << (8 * e);
             }
             dlo[j] = lo;
             dhi[j] = lo + 0x01010101u;  // d even: + 1 per byte, no carry
         }
     }
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
-    const int s_l = 2 * NW * (63 - l_eff);  // this lane's first staged entry
+    const int s_l = 2 * (63 - l_eff);  // this lane's first staged entry
     const int nout = y_end - y_begin;
     const int T = nout + 2 * RAD;
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
@@ -1190,9 +1197,14 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         int boff = (t & (NB - 1)) * C::NRS;
         asm volatile("" : "+s"(boff));
         const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
+        // The staged entries come in C::SPLIT batches of vector reads, each consumed by the chain
+        // steps it completes before the next batch is read (r = 7: fewer live VGPRs, so three
+        // waves fit per SIMD; the second batch's latency is covered by the other waves).
         uint32_t E[C::NE_V];
+        constexpr int NV = C::NE_V / C::VEC, NV1 = C::SPLIT > 1 ? (NV + 1) / 2 : NV;
+        constexpr int J1 = C::SPLIT > 1 ? NV1 * C::VEC - 1 : NPOS;  // steps the first batch completes
 #pragma unroll
-        for (int k = 0; k < C::NE_V / C::VEC; ++k) {
+        for (int k = 0; k < NV1; ++k) {
             const VT v = rb[k];
 #pragma unroll
             for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
@@ -1201,8 +1213,20 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         uint32_t A[NPOS + 1];
         A[0] = 0;
 #pragma unroll
-        for (int j = 0; j < NPOS; ++j)
+        for (int j = 0; j < J1; ++j)
             A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+        if constexpr (C::SPLIT > 1) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = NV1; k < NV; ++k) {
+                const VT v = rb[k];
+#pragma unroll
+                for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+            }
+#pragma unroll
+            for (int j = J1; j < NPOS; ++j)
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+        }
 #pragma unroll
         for (int x = 0; x < K; ++x) {
             const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
@@ -1249,12 +1273,21 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         uint32_t v[16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const uint4 q = reinterpret_cast<const uint4*>(tb)[rdw[j]];
+            // (r = 7: the second window's index is rebuilt per row as well)
+            const uint32_t ri = (C::SPLIT > 1 && j == 1) ? (rdw[0] ^ 1u) : rdw[j];
+            const uint4 q = reinterpret_cast<const uint4*>(tb)[ri];
             const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+            // (r = 7: the second window's d table and both d + 1 tables are rebuilt per row from
+            // dlo[0], three VGPRs fewer across the loop: bit 3 of every d byte is the window)
+            uint32_t dl = dlo[j], dh = dhi[j];
+            if constexpr (C::SPLIT > 1) {
+                dl = j == 0 ? dlo[0] : (dlo[0] ^ 0x08080808u);
+                dh = dl + 0x01010101u;
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                v[8 * j + 2 * e] = __builtin_amdgcn_perm(w4[e], dlo[j], 0x0c050400u + (uint32_t)e);
-                v[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w4[e], dhi[j], 0x0c070600u + (uint32_t)e);
+                v[8 * j + 2 * e] = __builtin_amdgcn_perm(w4[e], dl, 0x0c050400u + (uint32_t)e);
+                v[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w4[e], dh, 0x0c070600u + (uint32_t)e);
             }
         }
         asm volatile("" ::: "memory");
@@ -1267,7 +1300,13 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         m = min(m, dpp<kQuadSwap1>(m));
         m = min(m, dpp<kQuadSwap2>(m));
         m = min(m, dpp<kRowHalfMirror>(m));
-        comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 3)] = m;
+        int px = lane >> 3;
+        if constexpr (C::SPLIT > 1) {  // r = 7: rebuilt, not kept live through the row loop
+            px = threadIdx.x;
+            asm volatile("" : "+v"(px));
+            px = (px & 63) >> 3;
+        }
+        comb[((cb * KRB + slot) * NW + wave) * K + px] = m;
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -1301,7 +1340,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     wait_vmcnt<0>();
 }
 
-constexpr int pair_occ(int rad, int) { return rad >= 7 ? 2 : 3; }
+#ifndef USV_PAIR_OCC7
+#define USV_PAIR_OCC7 3  // waves per SIMD the r = 7 paired kernel is compiled for
+#endif
+constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : 3; }
 
 template <int RAD, int NW>
 __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
