@@ -62,8 +62,11 @@ def parse():
     p.add_argument("--split", choices=["pairs", "bands"], default="pairs",
                    help="N > 1: one pair per GPU (weak scaling, config D) or one frame split into row bands "
                         "with halos (strong scaling of config C, sharding.match_band)")
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget (N=1 only)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="CPU-baseline sample budget: warm-up + 5 timed runs share it (N=1 only)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--extra-steps", type=int, default=20,
+                   help="timed frames per extra leg (end-to-end, frame chain, generic fallbacks); 0 = skip")
     p.add_argument("--event-mode", choices=["sampled", "region", "per-step"], default="sampled",
                    help="kernel duration from HIP events around every --event-every-th launch of the timed "
                         "region (default), around every launch (adds ~6 us of wall time per step: each event "
@@ -103,8 +106,9 @@ def fast_kernel_name(W: int, D: int, w: int, pitch: int) -> str:
     return "sad_generic_kernel"
 
 
-def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float):
-    """Oracle (oracle/sad_oracle.c sliding variant, all allowed cores) on a bounded row band."""
+def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float, runs: int = 5):
+    """Oracle (oracle/sad_oracle.c sliding variant, all allowed cores) on a bounded row band of the
+    same pair: one warm-up run, then the median of `runs` timed runs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import load_oracle
 
@@ -122,17 +126,45 @@ def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float):
 
     probe = max(cores, 16)
     t = run(probe)
-    rows = int(min(H, max(probe, probe * budget_s / max(t, 1e-6) * 0.5)))
-    times = [run(rows) for _ in range(2)]
-    best = min(times)
+    rows = int(min(H, max(probe, probe * budget_s / (runs + 1) / max(t, 1e-6))))
+    run(rows)  # warm-up
+    times = [run(rows) for _ in range(runs)]
+    med = float(np.median(times))
     return {
-        "value": rows * W / best,
+        "value": rows * W / med,
         "unit": "disparity-pixels/s",
         "cores": cores,
         "kind": "port",
         "sample": f"oracle sliding-window SAD, rows 0..{rows} of the {W}x{H} w={w} D={D} pair "
-                  f"({rows * W} output pixels), best of {len(times)}",
+                  f"({rows * W} output pixels), median of {runs} runs after one warm-up",
+        "runs_s": times,
     }
+
+
+def cpu_naive_configs() -> dict:
+    """The naive single-thread oracle (definition-level triple loop, oracle/sad_oracle.c) on configs A
+    and B in full: median of 3 runs after a warm-up."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_oracle
+
+    lib = load_oracle()
+    res = {}
+    for name, (W, H, D, w) in {"A": (320, 240, 32, 5), "B": (640, 480, 64, 7)}.items():
+        L, R, _ = synthetic_pair(W, H, D, pair_index=0, noise=2)
+        out = np.zeros_like(L)
+
+        def run():
+            t0 = time.perf_counter()
+            assert lib.usv_oracle_sad_naive(L.ctypes.data, R.ctypes.data, W, H, W, D, w, 0, out.ctypes.data, W) == 0
+            return time.perf_counter() - t0
+
+        run()
+        times = [run() for _ in range(3)]
+        med = float(np.median(times))
+        res[name] = {"workload": f"{W}x{H} w={w} D={D}", "ms_per_pair": med * 1e3,
+                     "value": W * H / med, "unit": "disparity-pixels/s", "cores": 1, "kind": "port",
+                     "runs_s": times}
+    return res
 
 
 def time_launches(fn, steps: int, stream) -> float:
@@ -230,6 +262,93 @@ def plumbing_rehearsal(a, world: int, rank: int) -> None:
                           "max_rank_seen": int(t[1])}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def e2e_leg(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
+    """PCIe-inclusive frame time: pinned host pair -> device, match + distance map, u8 disparity
+    and f64 distance back to pinned host memory, one stream, synchronised per frame (the
+    reference's caller hands over host cv::Mat frames).  Never the headline value."""
+    matcher = StereoBlockMatcher(D, w)
+    H, W = L.shape
+    hl, hr = torch.from_numpy(L).pin_memory(), torch.from_numpy(R).pin_memory()
+    dl, dr = torch.empty((H, W), dtype=torch.uint8, device=dev), torch.empty((H, W), dtype=torch.uint8, device=dev)
+    hd = torch.empty((H, W), dtype=torch.uint8).pin_memory()
+    hx = torch.empty((H, W), dtype=torch.float64).pin_memory()
+    dd, dx = torch.empty_like(dl), torch.empty((H, W), dtype=torch.float64, device=dev)
+
+    def frame():
+        dl.copy_(hl, non_blocking=True)
+        dr.copy_(hr, non_blocking=True)
+        matcher.compute(dl, dr, with_distance=True, out_disp=dd, out_dist=dx)
+        hd.copy_(dd, non_blocking=True)
+        hx.copy_(dx, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    for _ in range(3):
+        frame()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        frame()
+    dt = (time.perf_counter() - t0) / steps
+    return {"ms_per_frame": dt * 1e3, "value": W * H / dt, "unit": "disparity-pixels/s",
+            "bytes_h2d": 2 * W * H, "bytes_d2h": 9 * W * H,
+            "note": "H2D (L, R) + fused matcher + D2H (u8 disparity, f64 distance), pinned host buffers, "
+                    "one stream, synchronised per frame; PCIe-inclusive, not the headline"}
+
+
+def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
+    """The real per-frame chain on the device: rectify both BGR frames (one launch) -> frame prep
+    of each camera (HSV, equalizeHist, BGR, gray) -> SAD block match of the rectified gray pair ->
+    fused distance map (P/Main.cpp:913-921 then the north-star matcher), synthetic calibration."""
+    from unsynchronized_stereo_vision_proj325_amd.preproc import FramePrep
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
+
+    rng = np.random.default_rng(11)
+    cl, cr = synthetic_calibration(W, H, seed=2)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)
+    pl, pr = FramePrep(dev), FramePrep(dev)
+    bufs = [(torch.empty_like(src_l), torch.empty_like(src_l), torch.empty((H, W), dtype=torch.uint8, device=dev))
+            for _ in range(2)]
+    disp = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    dist = torch.empty((H, W), dtype=torch.float64, device=dev)
+    matcher = StereoBlockMatcher(D, w)
+
+    def frame():
+        rectify_pair(rl, rr, src_l, src_r, rect_l, rect_r)
+        pl(rect_l, *bufs[0])
+        pr(rect_r, *bufs[1])
+        matcher.compute(bufs[0][2], bufs[1][2], with_distance=True, out_disp=disp, out_dist=dist)
+
+    us = time_launches(frame, steps, torch.cuda.current_stream())
+    return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
+            "stages": "rectify pair (BGR) -> frame prep x2 -> SAD w=%d D=%d -> distance map" % (w, D),
+            "launches_per_frame": 1 + 2 * 2 + 1}
+
+
+def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
+    """What the AUTO dispatch costs off the fast path: the direct-window generic kernel
+    (csrc/usv_sad_generic.hip, O(D w^2) per pixel) for SSD at the headline config, and for SAD on a
+    1918-wide (W % 4 != 0) crop of the same pair."""
+    s = torch.cuda.current_stream()
+    Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    out = {}
+    H, W = L.shape
+    ssd = StereoBlockMatcher(D, w, "ssd")
+    d1 = torch.empty_like(Lt)
+    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps, s)
+    out["ssd_generic"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
+    Lc, Rc = Lt[:, :1918], Rt[:, :1918]
+    sad = StereoBlockMatcher(D, w)
+    d2 = torch.empty((H, 1918), dtype=torch.uint8, device=dev)
+    us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), steps, s)
+    out["sad_generic_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
+                                "value": 1918 * H / (us * 1e-6)}
+    out["note"] = "generic kernel: one thread per pixel, direct window, no reuse; AUTO takes it for SSD and " \
+                  "for shapes outside the fast path (W % 4, W < 48, unaligned pitch)"
+    return out
 
 
 def main():
@@ -358,7 +477,7 @@ def main():
     bytes_per_px = 3 + (8 if with_dist else 0)  # L + R + u8 disparity (+ f64 distance)
     alg_bytes = bytes_per_px * rows * W  # this rank's launch (its halo'd band when split by bands)
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
-    workload_key = f"C_{W}x{H}_w{w}_D{D}_{'dist' if with_dist else 'nodist'}"
+    workload_key = f"{_config_name(W, H, w, D)}_{W}x{H}_w{w}_D{D}_{'dist' if with_dist else 'nodist'}"
     prof = None if bands else profile_counters(workload_key)  # counters were taken on whole frames
     kname = fast_kernel_name(W, D, w, W)
     rec = {
@@ -420,9 +539,14 @@ def main():
                            "note": "per-frame stages around the matcher, SURVEY.md 8(f) rows 1 and 3; "
                                    "HBM roofline per leg (algorithmic bytes / avg launch, HIP events)",
                            **pipeline_legs(dev, W, H, a.pipeline_steps)}
+    if world == 1 and rank == 0 and a.extra_steps > 0:
+        rec["e2e"] = e2e_leg(dev, L, R, D, w, a.extra_steps)
+        rec["frame_chain"] = frame_chain_leg(dev, W, H, D, w, a.extra_steps)
+        rec["fallbacks"] = fallback_legs(dev, L, R, D, w, max(2, a.extra_steps // 4))
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
         rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]
+        rec["cpu_naive"] = cpu_naive_configs()
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 ROUNDS=${ROUNDS:-3}
-ARGS=${ARGS:---steps 200 --warmup 20 --no-cpu-baseline}
+ARGS=${ARGS:---steps 200 --warmup 20 --no-cpu-baseline --extra-steps 0}
 out=gpurun_out/ab.txt; : > $out
 for r in $(seq $ROUNDS); do
   for v in default build_variants/*.so; do

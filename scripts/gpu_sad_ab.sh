@@ -2,4 +2,4 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_sad.log 2>&1 || { tail -30 gpurun_out/pytest_sad.log; exit 1; }
 tail -1 gpurun_out/pytest_sad.log
-ROUNDS=3 ARGS="--steps 200 --warmup 20 --no-cpu-baseline --pipeline-steps 0" bash scripts/ab_interleaved.sh
+ROUNDS=3 ARGS="--steps 200 --warmup 20 --no-cpu-baseline --pipeline-steps 0 --extra-steps 0" bash scripts/ab_interleaved.sh

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
-ARGS=${*:---steps 20 --warmup 5 --no-cpu-baseline}
+ARGS=${*:---steps 20 --warmup 5 --no-cpu-baseline --extra-steps 0}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; [ "$1" -gt 128 ] && return 0; return 1; }
