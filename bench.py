@@ -71,7 +71,7 @@ def parse():
                    help="kernel duration from HIP events around every --event-every-th launch of the timed "
                         "region (default), around every launch (adds ~6 us of wall time per step: each event "
                         "pair serialises the stream), or the region span / steps")
-    p.add_argument("--event-every", type=int, default=8)
+    p.add_argument("--event-every", type=int, default=8, help="upper bound; at most steps/8 (>= 8 samples)")
     p.add_argument("--pipeline-steps", type=int, default=50,
                    help="timed launches per pipeline leg (rectify / frame prep / mask); 0 = skip")
     return p.parse_args()
@@ -452,7 +452,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    every = 1 if a.event_mode == "per-step" else max(1, a.event_every)
+    # sampled: every k-th launch, k <= steps / 8 so that short runs (the driver's --steps 20) still time
+    # >= 8 launches (each sampled pair of events costs a few us of wall time, so not every launch)
+    every = 1 if a.event_mode == "per-step" else max(1, min(a.event_every, a.steps // 8))
     timed = [i for i in range(a.steps) if i % every == every // 2] if a.event_mode != "region" else []
     events = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed}
     span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
