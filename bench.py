@@ -335,25 +335,28 @@ def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
 
 
 def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
-    """What the AUTO dispatch costs off the fast path: the direct-window generic kernel
-    (csrc/usv_sad_generic.hip, O(D w^2) per pixel) for SSD at the headline config, and for SAD on a
-    1918-wide (W % 4 != 0) crop of the same pair."""
+    """What the AUTO dispatch costs off the fast SAD kernels: the tiled sliding-window kernel
+    (csrc/usv_sad_tiled.hip) for SSD at the headline config and for SAD on a 1918-wide (W % 4 != 0)
+    crop of the same pair, and the direct-window generic kernel (csrc/usv_sad_generic.hip,
+    O(D w^2) per pixel, what AUTO ran for these shapes before the tiled kernel) beside them."""
     s = torch.cuda.current_stream()
     Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
     out = {}
     H, W = L.shape
-    ssd = StereoBlockMatcher(D, w, "ssd")
     d1 = torch.empty_like(Lt)
-    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps, s)
-    out["ssd_generic"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
-    Lc, Rc = Lt[:, :1918], Rt[:, :1918]
-    sad = StereoBlockMatcher(D, w)
     d2 = torch.empty((H, 1918), dtype=torch.uint8, device=dev)
-    us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), steps, s)
-    out["sad_generic_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
-                                "value": 1918 * H / (us * 1e-6)}
-    out["note"] = "generic kernel: one thread per pixel, direct window, no reuse; AUTO takes it for SSD and " \
-                  "for shapes outside the fast path (W % 4, W < 48, unaligned pitch)"
+    Lc, Rc = Lt[:, :1918], Rt[:, :1918]
+    for kernel, n in (("tiled", steps * 8), ("generic", steps)):
+        ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)
+        us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s)
+        out[f"ssd_{kernel}"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
+        sad = StereoBlockMatcher(D, w, kernel=kernel)
+        us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s)
+        out[f"sad_{kernel}_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
+                                      "value": 1918 * H / (us * 1e-6)}
+    out["note"] = "AUTO runs the tiled kernel (vertical running sums, LDS-DMA row ring) for SSD and for shapes " \
+                  "outside the fast SAD kernels (W % 4, W < 48, unaligned pitch or base); generic = one thread " \
+                  "per pixel, direct window, now only for w > 31"
     return out
 
 

@@ -83,9 +83,10 @@ typedef enum {
 } usv_distance_model;
 
 typedef enum {
-    USV_KERNEL_AUTO = 0,   /* fast path when the shape allows it, else generic */
-    USV_KERNEL_FAST = 1,   /* lane-per-disparity running-sum kernel; UNSUPPORTED if not applicable */
-    USV_KERNEL_GENERIC = 2 /* direct-window kernel, any w <= 63, SAD or SSD */
+    USV_KERNEL_AUTO = 0,    /* fast SAD path when the shape allows it, else tiled, else generic */
+    USV_KERNEL_FAST = 1,    /* lane-per-disparity packed running-sum SAD kernels; UNSUPPORTED if not applicable */
+    USV_KERNEL_GENERIC = 2, /* direct-window kernel, any w <= 63, SAD or SSD (reference-speed fallback) */
+    USV_KERNEL_TILED = 3    /* sliding-window kernel: SAD or SSD, any W / pitch / alignment, w <= 31 */
 } usv_kernel;
 
 /* Library / device info. */

@@ -93,17 +93,25 @@ usv_status validate(const usv::MatchArgs& a) {
 usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
     usv_status st = validate(a);
     if (st != USV_OK) return st;
-    if (kernel != USV_KERNEL_AUTO && kernel != USV_KERNEL_FAST && kernel != USV_KERNEL_GENERIC)
+    if (kernel != USV_KERNEL_AUTO && kernel != USV_KERNEL_FAST && kernel != USV_KERNEL_GENERIC &&
+        kernel != USV_KERNEL_TILED)
         return USV_ERR_INVALID_ARG;
     if (kernel == USV_KERNEL_FAST && !usv::fast_path_supported(a)) return USV_ERR_UNSUPPORTED;
+    if (kernel == USV_KERNEL_TILED && !usv::tiled_path_supported(a)) return USV_ERR_UNSUPPORTED;
     if (a.dist && (st = resolve_lut(a.lut, &a.lut)) != USV_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (kernel) {
         case USV_KERNEL_AUTO:
-            return to_status(usv::fast_path_supported(a) ? usv::launch_fast(a, s) : usv::launch_generic(a, s));
+            // fast SAD kernels, else the tiled sliding-window kernel (SSD, any shape, w <= 31),
+            // else the direct-window kernel (w > 31, or a window too large for the tiled ring)
+            if (usv::fast_path_supported(a)) return to_status(usv::launch_fast(a, s));
+            if (usv::tiled_path_supported(a)) return to_status(usv::launch_tiled(a, s));
+            return to_status(usv::launch_generic(a, s));
         case USV_KERNEL_FAST:
             if (!usv::fast_path_supported(a)) return USV_ERR_UNSUPPORTED;
             return to_status(usv::launch_fast(a, s));
+        case USV_KERNEL_TILED:
+            return to_status(usv::launch_tiled(a, s));
         case USV_KERNEL_GENERIC:
             return to_status(usv::launch_generic(a, s));
         default:

@@ -28,6 +28,11 @@ struct MatchArgs {
 bool fast_path_supported(const MatchArgs& a);
 hipError_t launch_fast(const MatchArgs& a, hipStream_t s);
 
+// Tiled sliding-window path: SAD or SSD, any W / pitch / alignment, odd w <= 31
+// (usv_sad_tiled.hip).  Returns hipErrorInvalidValue outside that range.
+bool tiled_path_supported(const MatchArgs& a);
+hipError_t launch_tiled(const MatchArgs& a, hipStream_t s);
+
 // Generic direct-window path: any odd w <= 63, SAD or SSD (usv_sad_generic.hip).
 hipError_t launch_generic(const MatchArgs& a, hipStream_t s);
 
