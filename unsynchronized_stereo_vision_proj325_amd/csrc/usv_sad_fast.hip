@@ -1058,6 +1058,10 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 // 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
 // rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
 // ===================================================================================
+#ifndef USV_PEXP
+#define USV_PEXP 0  // timing experiments (wrong results): 1 no per-row L load, 2 also no L-byte extraction,
+                   // 3 no argmin transpose, 4 no steady-state R DMA, 5 half chain, 6 no ring subtraction
+#endif
 template <int RAD, int NW>
 struct PCfg {
     static constexpr int K = 8;
@@ -1173,6 +1177,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         __builtin_amdgcn_wave_barrier();
         if constexpr (WARM) {
             issue_dma(t + PD);
+        } else if constexpr (USV_PEXP == 4) {
         } else {
             int rr = rawR;
             asm volatile("" : "+s"(rr));
@@ -1189,7 +1194,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
             for (int j = 0; j < NPOS; ++j) {
                 const int bidx = LS::byte(j);
-                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+                if (USV_PEXP == 2) Lv[j] = lw[(bidx >> 2) & 7];  // timing experiment: no extraction (wrong)
+                else if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
                 else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
@@ -1214,7 +1220,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         A[0] = 0;
 #pragma unroll
         for (int j = 0; j < J1; ++j)
-            A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+            A[j + 1] = USV_PEXP == 5 ? __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j])
+                                     : __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
         if constexpr (C::SPLIT > 1) {
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1230,13 +1237,15 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
         for (int x = 0; x < K; ++x) {
             const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
-            if constexpr (WARM) S[x] = S[x] + h;
+            if constexpr (WARM || USV_PEXP == 6) S[x] = S[x] + h;
             else S[x] = (S[x] - ring[I][x]) + h;
             ring[I][x] = h;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (WARM) {
             load_lw(t + 1);
+        } else if constexpr (USV_PEXP == 1 || USV_PEXP == 2) {
+            // timing experiment: L row segment loaded once per band (wrong results)
         } else {
             int rl = rawL;
             asm volatile("" : "+s"(rl));
@@ -1267,6 +1276,11 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         cb ^= 1;
     };
     auto emit = [&](const uint32_t(&S)[K], int slot) {
+        if constexpr (USV_PEXP == 3) {
+            comb[((cb * KRB + slot) * NW + wave) * K + (lane & 7)] = S[0] ^ S[1] ^ S[2] ^ S[3] ^ S[4] ^ S[5] ^ S[6] ^ S[7];
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
         asm volatile("" ::: "memory");
@@ -1497,6 +1511,9 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
     if (!fast_path_supported(a)) return hipErrorInvalidValue;
 #ifdef USV_DEV_ONLY_RAD  // development: build a single instantiation for ISA inspection
     return launch_rn<USV_DEV_ONLY_RAD, USV_DEV_ONLY_NW>(a, s);
+#elif defined(USV_EXP_PAIR_ONLY)  // timing experiments: the paired kernel only (configs C and E)
+    if (!pair_path_supported(a)) return hipErrorInvalidValue;
+    return a.w == 11 ? launch_pair_r<5>(a, s) : a.w == 15 ? launch_pair_r<7>(a, s) : hipErrorInvalidValue;
 #else
     if (pair_path_supported(a)) {
         switch ((a.w - 1) / 2) {
