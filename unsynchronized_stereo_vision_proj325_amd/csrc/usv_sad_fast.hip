@@ -1058,6 +1058,14 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 // 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
 // rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
 // ===================================================================================
+#ifndef USV_PAIR_PIPE
+#define USV_PAIR_PIPE 1  // argmin transpose of row t finished during row t + 1 (latency hidden by the chain)
+#endif
+#ifndef USV_PAIR_PIPE_R7
+#define USV_PAIR_PIPE_R7 0  // experiment: pipelined argmin at r = 7 (needs USV_PAIR_OCC7=2, USV_PAIR_SPLIT_R=8)
+#endif
+template <int RAD>
+constexpr bool kPairPipe = USV_PAIR_PIPE && (RAD == 5 || (RAD == 7 && USV_PAIR_PIPE_R7));
 #ifndef USV_PEXP
 #define USV_PEXP 0  // timing experiments (wrong results): 1 no per-row L load, 2 also no L-byte extraction,
                    // 3 no argmin transpose, 4 no steady-state R DMA, 5 half chain, 6 no ring subtraction
@@ -1090,6 +1098,26 @@ struct PCfg {
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
 };
+
+// The paired kernel's L row segment lives in FIXED SGPRs s[40:45] from its scalar load to the wait
+// that retires it: with ordinary "s" constraints the register allocator may copy the in-flight
+// destination into other SGPRs before the wait (seen at loop latches), reading stale words.
+template <int N>
+__device__ __forceinline__ typename SWords<N>::T s_load_words_pin(const uint8_t* p, uint32_t off) {
+    static_assert(N == 4 || N == 6, "paired kernel segments are 4 or 6 dwords");
+    typename SWords<N>::T w;
+    if constexpr (N == 4)
+        asm volatile("s_load_dwordx4 %0, %1, %2" : "=&{s[40:43]}"(w) : "s"(p), "s"(off) : "memory");
+    else
+        asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dwordx2 %1, %2, %3 offset:0x10"
+                     : "=&{s[40:43]}"(w.a), "=&{s[44:45]}"(w.b) : "s"(p), "s"(off) : "memory");
+    return w;
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm0_pin(typename SWords<N>::T& w) {
+    if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:43]}"(w) : : "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:43]}"(w.a), "+{s[44:45]}"(w.b) : : "memory");
+}
 
 template <int RAD, int NW, int EDGE>
 __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
@@ -1166,9 +1194,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
     };
     LWords lw_next;
-    auto load_lw = [&](int t) { lw_next = s_load_words<LS::NLD>(Lseg + row_off(t)); };
+    auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
 
-    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
+    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int I = decltype(i_tag)::value;
         int t = t_in;
@@ -1185,10 +1213,17 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
             rawR = rr + a.pitch;
         }
+        // (pipelined argmin: the ring row leaving the window is subtracted first, so its registers
+        // are free for this row's staged entries -- no copies)
+        constexpr bool EARLY_SUB = !WARM && kPairPipe<RAD> && USV_PEXP != 6;
+        if constexpr (EARLY_SUB) {
+#pragma unroll
+            for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        }
         uint32_t Lv[NPOS];
         {
+            wait_lgkm0_pin<LS::NLD>(lw_next);
             LWords cur = lw_next;
-            wait_lgkm0<LS::NLD>(cur);
             uint32_t lw[8];
             unpack_words<LS::NLD>(cur, lw);
 #pragma unroll
@@ -1199,6 +1234,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
+        auto lbyte = [&](int j) -> uint32_t { return Lv[j]; };
         using VT = typename VecT<C::VEC>::T;
         int boff = (t & (NB - 1)) * C::NRS;
         asm volatile("" : "+s"(boff));
@@ -1215,13 +1251,22 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
             for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
         }
-        // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half)
+        // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half).  With the argmin
+        // pipelined, piece j of the previous row's argmin follows chain step j and the pair is
+        // fenced: the two independent dependency chains interleave instruction by instruction.
         uint32_t A[NPOS + 1];
         A[0] = 0;
-#pragma unroll
-        for (int j = 0; j < J1; ++j)
-            A[j + 1] = USV_PEXP == 5 ? __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j])
-                                     : __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+        auto chain_step = [&](auto jt) {
+            constexpr int j = decltype(jt)::value;
+            const uint32_t l = lbyte(j);
+            A[j + 1] = USV_PEXP == 5 ? __builtin_amdgcn_sad_u8(l, E[j + 1], A[j])
+                                     : __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            pre(jt);
+            if constexpr (EARLY_SUB) __builtin_amdgcn_sched_barrier(0);
+        };
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (chain_step(std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, J1>{});
         if constexpr (C::SPLIT > 1) {
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1232,12 +1277,12 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             }
 #pragma unroll
             for (int j = J1; j < NPOS; ++j)
-                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(lbyte(j), E[j], __builtin_amdgcn_sad_u8(lbyte(j), E[j + 1], A[j]));
         }
 #pragma unroll
         for (int x = 0; x < K; ++x) {
             const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
-            if constexpr (WARM || USV_PEXP == 6) S[x] = S[x] + h;
+            if constexpr (WARM || EARLY_SUB || USV_PEXP == 6) S[x] = S[x] + h;
             else S[x] = (S[x] - ring[I][x]) + h;
             ring[I][x] = h;
         }
@@ -1249,7 +1294,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         } else {
             int rl = rawL;
             asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_off<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
             rawL = rl + a.pitch;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1275,22 +1320,41 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         y_chunk += rows;
         cb ^= 1;
     };
-    auto emit = [&](const uint32_t(&S)[K], int slot) {
-        if constexpr (USV_PEXP == 3) {
-            comb[((cb * KRB + slot) * NW + wave) * K + (lane & 7)] = S[0] ^ S[1] ^ S[2] ^ S[3] ^ S[4] ^ S[5] ^ S[6] ^ S[7];
-            __builtin_amdgcn_sched_barrier(0);
+    // Argmin of one row, in two halves so that the LDS round trip of the transpose and the
+    // dependent min / DPP tail overlap the next row's chain (USV_PAIR_PIPE):
+    //   tr_issue:  lane l stores its 8 packed words, lane 8p + q reads the 8 words of pixel p from
+    //              lanes 8q .. 8q + 7 (two ds_read_b128) -- nothing waits on them here;
+    //   tr_finish: 16 keys (cost << 8) | d by v_perm, a v_min3 tree, three DPP rounds across the 8
+    //              lanes of the pixel, one comb word per pixel.
+    uint4 trq[2];
+    auto tr_issue = [&](const uint32_t(&S)[K]) {
+        if constexpr (USV_PEXP == 7) {  // timing experiment: no LDS transpose (wrong results)
+            trq[0] = make_uint4(S[0], S[1], S[2], S[3]);
+            trq[1] = make_uint4(S[4], S[5], S[6], S[7]);
             return;
         }
 #pragma unroll
         for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
         asm volatile("" ::: "memory");
-        uint32_t v[16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             // (r = 7: the second window's index is rebuilt per row as well)
             const uint32_t ri = (C::SPLIT > 1 && j == 1) ? (rdw[0] ^ 1u) : rdw[j];
-            const uint4 q = reinterpret_cast<const uint4*>(tb)[ri];
-            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+            trq[j] = reinterpret_cast<const uint4*>(tb)[ri];
+        }
+        asm volatile("" ::: "memory");
+    };
+    // tr_finish in 16 pieces (piece J after chain step J of the next row when pipelined)
+    uint32_t fv[16], fb[5], fm;
+    auto tr_piece = [&](auto jt, int slot) {
+        constexpr int J = decltype(jt)::value;
+        if constexpr (USV_PEXP == 8) {  // timing experiment: transpose kept, key / min VALU skipped (wrong)
+            if constexpr (J == 15)
+                comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 3)] =
+                    trq[0].x ^ trq[0].y ^ trq[0].z ^ trq[0].w ^ trq[1].x ^ trq[1].y ^ trq[1].z ^ trq[1].w;
+        } else if constexpr (J < 8) {
+            constexpr int j = J >> 2, e = J & 3;
+            const uint32_t w = e == 0 ? trq[j].x : e == 1 ? trq[j].y : e == 2 ? trq[j].z : trq[j].w;
             // (r = 7: the second window's d table and both d + 1 tables are rebuilt per row from
             // dlo[0], three VGPRs fewer across the loop: bit 3 of every d byte is the window)
             uint32_t dl = dlo[j], dh = dhi[j];
@@ -1298,31 +1362,47 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 dl = j == 0 ? dlo[0] : (dlo[0] ^ 0x08080808u);
                 dh = dl + 0x01010101u;
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[8 * j + 2 * e] = __builtin_amdgcn_perm(w4[e], dl, 0x0c050400u + (uint32_t)e);
-                v[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w4[e], dh, 0x0c070600u + (uint32_t)e);
+            fv[8 * j + 2 * e] = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
+            fv[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
+        } else if constexpr (J == 8) {
+            fb[0] = min(min(fv[0], fv[1]), fv[2]);
+            fb[1] = min(min(fv[3], fv[4]), fv[5]);
+        } else if constexpr (J == 9) {
+            fb[2] = min(min(fv[6], fv[7]), fv[8]);
+            fb[3] = min(min(fv[9], fv[10]), fv[11]);
+        } else if constexpr (J == 10) {
+            fb[4] = min(min(fv[12], fv[13]), fv[14]);
+            fb[0] = min(min(fb[0], fb[1]), fb[2]);
+        } else if constexpr (J == 11) {
+            fb[3] = min(min(fb[3], fb[4]), fv[15]);
+            fm = min(fb[0], fb[3]);
+        } else if constexpr (J == 12) {
+            fm = min(fm, dpp<kQuadSwap1>(fm));
+        } else if constexpr (J == 13) {
+            fm = min(fm, dpp<kQuadSwap2>(fm));
+        } else if constexpr (J == 14) {
+            fm = min(fm, dpp<kRowHalfMirror>(fm));
+        } else if constexpr (J == 15) {
+            int px = lane >> 3;
+            if constexpr (C::SPLIT > 1) {  // r = 7: rebuilt, not kept live through the row loop
+                px = threadIdx.x;
+                asm volatile("" : "+v"(px));
+                px = (px & 63) >> 3;
             }
+            comb[((cb * KRB + slot) * NW + wave) * K + px] = fm;
         }
-        asm volatile("" ::: "memory");
-        uint32_t b0 = min(min(v[0], v[1]), v[2]), b1 = min(min(v[3], v[4]), v[5]);
-        uint32_t b2 = min(min(v[6], v[7]), v[8]), b3 = min(min(v[9], v[10]), v[11]);
-        uint32_t b4 = min(min(v[12], v[13]), v[14]);
-        b0 = min(min(b0, b1), b2);
-        b3 = min(min(b3, b4), v[15]);
-        uint32_t m = min(b0, b3);
-        m = min(m, dpp<kQuadSwap1>(m));
-        m = min(m, dpp<kQuadSwap2>(m));
-        m = min(m, dpp<kRowHalfMirror>(m));
-        int px = lane >> 3;
-        if constexpr (C::SPLIT > 1) {  // r = 7: rebuilt, not kept live through the row loop
-            px = threadIdx.x;
-            asm volatile("" : "+v"(px));
-            px = (px & 63) >> 3;
-        }
-        comb[((cb * KRB + slot) * NW + wave) * K + px] = m;
+    };
+    auto tr_finish = [&](int slot) {
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (tr_piece(std::integral_constant<int, J>{}, slot), ...);
+        }(std::make_integer_sequence<int, 16>{});
+    };
+    auto emit = [&](const uint32_t(&S)[K], int slot) {
+        tr_issue(S);
+        tr_finish(slot);
         __builtin_amdgcn_sched_barrier(0);
     };
+    auto no_pre = [](auto) {};
 
     uint32_t S[K];
 #pragma unroll
@@ -1333,14 +1413,35 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     using WarmT = std::integral_constant<bool, true>;
     using SteadyT = std::integral_constant<bool, false>;
     [&]<int... I>(std::integer_sequence<int, I...>) {
-        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
+        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring, no_pre), ...);
     }(std::make_integer_sequence<int, WIN>{});
-    emit(S, 0);
+    // Pipelined argmin (PIPE): output row k is slot k % KRB.  Row k's transpose is issued after its
+    // chain and finished inside the next row's do_row (after that row's staged reads are issued), so
+    // slot I is pending when the I-th row of a WIN-row group starts; the chunk is flushed once slot
+    // KRB - 1 is finished.  (r = 6, 7 keep the unpipelined order: the held transpose words spill.)
+    constexpr bool PIPE = kPairPipe<RAD>;
+    static_assert(KRB == WIN, "pending slot = row index in the unrolled group");
+    static_assert(!PIPE || NPOS >= 16, "16 argmin pieces ride on the chain steps");
+    if constexpr (PIPE) {
+        tr_issue(S);
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+        emit(S, 0);
+    }
     auto step = [&](int t0, auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
-        do_row(t0 + I, SteadyT{}, i_tag, S, ring);
-        emit(S, (I + 1) % WIN);
-        if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+        if constexpr (PIPE) {
+            do_row(t0 + I, SteadyT{}, i_tag, S, ring, [&](auto jt) {
+                if constexpr (decltype(jt)::value < 16) tr_piece(jt, I);
+            });
+            if constexpr (I == KRB - 1) flush(KRB);
+            tr_issue(S);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            do_row(t0 + I, SteadyT{}, i_tag, S, ring, no_pre);
+            emit(S, (I + 1) % WIN);
+            if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+        }
     };
     for (int t0 = WIN; t0 < T; t0 += WIN) {
         [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -1348,7 +1449,12 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
         }(std::make_integer_sequence<int, WIN>{});
     }
-    wait_lgkm0<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
+    wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
+    if constexpr (PIPE) {
+        const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
+        tr_finish(last);
+        if (last == KRB - 1) flush(KRB);
+    }
     const int rest = nout % KRB;
     if (rest) flush(rest);
     wait_vmcnt<0>();
