@@ -1061,6 +1061,9 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 #ifndef USV_PAIR_PIPE
 #define USV_PAIR_PIPE 1  // argmin transpose of row t finished during row t + 1 (latency hidden by the chain)
 #endif
+#ifndef USV_WIDE_FLUSH
+#define USV_WIDE_FLUSH 1  // paired kernel: one 8-byte disparity store and one 16-byte distance store per lane per chunk
+#endif
 #ifndef USV_PAIR_PIPE_R7
 #define USV_PAIR_PIPE_R7 0  // experiment: pipelined argmin at r = 7 (needs USV_PAIR_OCC7=2, USV_PAIR_SPLIT_R=8)
 #endif
@@ -1201,7 +1204,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         constexpr int I = decltype(i_tag)::value;
         int t = t_in;
         asm volatile("" : "+s"(t));
-        wait_vmcnt<(PD - 1) * NDMA>();
+        wait_vmcnt<(PD - 1) * NDMA + (USV_PEXP == 11 ? 4 : 0)>();  // 11: timing experiment (unsafe)
         __builtin_amdgcn_wave_barrier();
         if constexpr (WARM) {
             issue_dma(t + PD);
@@ -1301,11 +1304,54 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     };
 
     int cb = 0, y_chunk = y_begin;
+    // Wide flush (USV_WIDE_FLUSH): a chunk's outputs leave in two store instructions -- lane r
+    // writes row r's 8 disparity bytes as one 8-byte store, lane 4r + q row r's distances 2q, 2q+1
+    // as one 16-byte store -- instead of a byte + a double per lane and item (4 per 11-row chunk).
+    // Global stores count in vmcnt on gfx9 with the LDS-DMA look-ahead, so fewer, wider stores also
+    // hold up fewer of the next rows' counted DMA waits.  Needs 4-byte aligned disparity rows.
+    const bool wide = USV_WIDE_FLUSH && ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
     auto flush = [&](int rows) {
         if constexpr (NW > 1) lds_barrier();
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
+        if (wide) {
+            static_assert(K == 8, "one 8-byte disparity store per row");
+            const uint32_t* crow = comb + (cb * KRB) * NW * K;
+            if (tid < rows) {
+                uint4 k0 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[0];
+                uint4 k1 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[1];
+#pragma unroll
+                for (int w2 = 1; w2 < NW; ++w2) {
+                    const uint4 m0 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[0];
+                    const uint4 m1 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[1];
+                    k0 = make_uint4(min(k0.x, m0.x), min(k0.y, m0.y), min(k0.z, m0.z), min(k0.w, m0.w));
+                    k1 = make_uint4(min(k1.x, m1.x), min(k1.y, m1.y), min(k1.z, m1.z), min(k1.w, m1.w));
+                }
+                // byte 0 of each key is its disparity
+                const uint32_t lo = __builtin_amdgcn_perm(k0.y, k0.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k0.w, k0.z, 0x04000c0cu);
+                const uint32_t hi = __builtin_amdgcn_perm(k1.y, k1.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k1.w, k1.z, 0x04000c0cu);
+                const size_t y = (size_t)(y_chunk + tid);
+                if (!(USV_PEXP == 10 && y != 0x7FFFFFFF))
+                    *reinterpret_cast<uint2*>(disp + y * a.disp_pitch + x0) = make_uint2(lo, hi);
+            }
+            if (dist && tid < 4 * rows) {
+                struct __attribute__((aligned(8))) D2 { double a, b; };
+                const int r = tid >> 2, q = tid & 3;
+                uint2 kk = reinterpret_cast<const uint2*>(crow + r * NW * K)[q];
+#pragma unroll
+                for (int w2 = 1; w2 < NW; ++w2) {
+                    const uint2 m = reinterpret_cast<const uint2*>(crow + (r * NW + w2) * K)[q];
+                    kk = make_uint2(min(kk.x, m.x), min(kk.y, m.y));
+                }
+                const size_t y = (size_t)(y_chunk + r);
+                if (!(USV_PEXP == 10 && y != 0x7FFFFFFF))
+                    *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+            }
+            y_chunk += rows;
+            cb ^= 1;
+            return;
+        }
         const int items = rows * K;
         for (int i = tid; i < items; i += NW * 64) {
             const int row = i / K, p = i - row * K;
@@ -1314,6 +1360,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
             const uint32_t dv = key & 0xFFu;
             const size_t y = (size_t)(y_chunk + row);
+            if (USV_PEXP == 10 && y != 0x7FFFFFFF) continue;  // timing experiment: no output stores (wrong)
             disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
             if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
         }
@@ -1364,6 +1411,19 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             }
             fv[8 * j + 2 * e] = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
             fv[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
+        } else if constexpr (USV_PEXP == 9 && J >= 8 && J <= 11) {  // experiment: two-operand min tree
+            if constexpr (J == 8) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) fv[i] = min(fv[i], fv[i + 8]);
+            } else if constexpr (J == 9) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) fv[i] = min(fv[i], fv[i + 4]);
+            } else if constexpr (J == 10) {
+                fv[0] = min(fv[0], fv[2]);
+                fv[1] = min(fv[1], fv[3]);
+            } else {
+                fm = min(fv[0], fv[1]);
+            }
         } else if constexpr (J == 8) {
             fb[0] = min(min(fv[0], fv[1]), fv[2]);
             fb[1] = min(min(fv[3], fv[4]), fv[5]);
@@ -1463,7 +1523,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #ifndef USV_PAIR_OCC7
 #define USV_PAIR_OCC7 3  // waves per SIMD the r = 7 paired kernel is compiled for
 #endif
-constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : 3; }
+#ifndef USV_PAIR_OCC5
+#define USV_PAIR_OCC5 3  // waves per SIMD the r <= 6 paired kernel is compiled for
+#endif
+constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : USV_PAIR_OCC5; }
 
 template <int RAD, int NW>
 __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
