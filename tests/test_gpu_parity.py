@@ -134,6 +134,38 @@ def test_pitched_views(gpu):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("dcol,dist_pitch", [(0, 261), (1, 261), (2, 263), (4, 264)])
+def test_pair_kernel_pitched_outputs(gpu, dcol, dist_pitch):
+    """Paired kernel (D > 64, w = 11): a chunk leaves as one 8-byte disparity store and one 16-byte
+    distance store per lane when the disparity rows are 4-byte aligned (dcol 0 / 4), else as byte
+    stores (dcol 1 / 2); distance rows at odd / even pitch.  Views into larger buffers: nothing outside
+    the view may be written."""
+    W, H, D, w = 240, 97, 96, 11
+    L, R, _ = synthetic_pair(W, H, D, pair_index=5, noise=2)
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    big_disp = torch.full((H + 2, 260), 77, dtype=torch.uint8, device=gpu)
+    out_disp = big_disp[1:H + 1, dcol:dcol + W]
+    big_dist = torch.full((H + 2, dist_pitch), -1.0, dtype=torch.float64, device=gpu)
+    out_dist = big_dist[1:H + 1, 3:3 + W]
+    m = StereoBlockMatcher(D, w)
+    m.compute(torch.from_numpy(L).to(gpu), torch.from_numpy(R).to(gpu), with_distance=True,
+              out_disp=out_disp, out_dist=out_dist)
+    torch.cuda.synchronize()
+    got = out_disp.cpu().numpy()
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    lut = distance_lut_cm()
+    dd = out_dist.cpu().numpy()
+    assert ((dd == lut[got]) | (np.isinf(dd) & np.isinf(lut[got]))).all()
+    bd = big_disp.cpu().numpy()
+    outside = np.ones(bd.shape, bool)
+    outside[1:H + 1, dcol:dcol + W] = False
+    assert (bd[outside] == 77).all()
+    bf = big_dist.cpu().numpy()
+    outside = np.ones(bf.shape, bool)
+    outside[1:H + 1, 3:3 + W] = False
+    assert (bf[outside] == -1.0).all()
+
+
 def test_batch_launch(gpu):
     pairs = [synthetic_pair(333, 97, 100, pair_index=i) for i in range(3)]
     L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
