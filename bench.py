@@ -334,6 +334,58 @@ def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
             "launches_per_frame": 1 + 2 * 2 + 1}
 
 
+def frame_chain_graph_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
+    """The same per-frame chain replayed as one HIP graph: the two cameras' frame prep forked onto a
+    second stream inside the graph (they are independent until the matcher), two frames per graph so
+    the frame-prep workspaces alternate their histogram parity as in eager use.  Checked against the
+    eager chain on the same input (disparity and distance maps bit-identical)."""
+    from unsynchronized_stereo_vision_proj325_amd.preproc import FramePrep
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
+
+    rng = np.random.default_rng(11)
+    cl, cr = synthetic_calibration(W, H, seed=2)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)
+    pl, pr = FramePrep(dev), FramePrep(dev)
+    bufs = [(torch.empty_like(src_l), torch.empty_like(src_l), torch.empty((H, W), dtype=torch.uint8, device=dev))
+            for _ in range(2)]
+    disp = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    dist = torch.empty((H, W), dtype=torch.float64, device=dev)
+    matcher = StereoBlockMatcher(D, w)
+    side = torch.cuda.Stream(dev)
+
+    def frame():
+        main = torch.cuda.current_stream()
+        rectify_pair(rl, rr, src_l, src_r, rect_l, rect_r)
+        side.wait_stream(main)
+        pl(rect_l, *bufs[0])
+        with torch.cuda.stream(side):
+            pr(rect_r, *bufs[1])
+        main.wait_stream(side)
+        matcher.compute(bufs[0][2], bufs[1][2], with_distance=True, out_disp=disp, out_dist=dist)
+
+    for _ in range(4):  # eager warm-up (lazy tables, occupancy queries); even count keeps the parities aligned
+        frame()
+    torch.cuda.synchronize()
+    ref_disp, ref_dist = disp.clone(), dist.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        frame()
+        frame()
+    disp.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(disp, ref_disp) and torch.equal(dist.nan_to_num(), ref_dist.nan_to_num()))
+    reps = max(2, steps // 2)
+    us = time_launches(g.replay, reps, torch.cuda.current_stream()) / 2
+    return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
+            "stages": "one hipGraph per two frames: rectify pair -> frame prep L || frame prep R (two streams) "
+                      "-> SAD w=%d D=%d -> distance map" % (w, D),
+            "matches_eager": same}
+
+
 def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
     """What the AUTO dispatch costs off the fast SAD kernels: the tiled sliding-window kernel
     (csrc/usv_sad_tiled.hip) for SSD at the headline config and for SAD on a 1918-wide (W % 4 != 0)
@@ -553,6 +605,7 @@ def main():
     if world == 1 and rank == 0 and a.extra_steps > 0:
         rec["e2e"] = e2e_leg(dev, L, R, D, w, a.extra_steps)
         rec["frame_chain"] = frame_chain_leg(dev, W, H, D, w, a.extra_steps)
+        rec["frame_chain_graph"] = frame_chain_graph_leg(dev, W, H, D, w, a.extra_steps)
         rec["fallbacks"] = fallback_legs(dev, L, R, D, w, max(2, a.extra_steps // 4))
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
