@@ -24,8 +24,12 @@ namespace usv {
 namespace {
 
 constexpr int kHsvShift = 12;
+#ifndef USV_PREP_FAST
+#define USV_PREP_FAST 1  // equalize: wave-level LUT scan (2 barriers instead of 16), single-step hue wrap
+#endif
 #ifndef USV_PREP_EXP
-#define USV_PREP_EXP 0  // timing experiments only (wrong histograms): 1 no global bin atomics, 2 no LDS atomics, 3 neither
+#define USV_PREP_EXP 0  // timing experiments only (wrong results): 1 no global bin atomics, 2 no LDS atomics, 3 neither,
+                        // 4 identity LUT, 8 no HSV2BGR, 16 no HSV table build
 #endif
 
 __device__ __forceinline__ void bgr2hsv_px(int b, int g, int r, const int* sdiv, const int* hdiv, int& h, int& s,
@@ -51,6 +55,29 @@ __device__ void hsv_tables(int* sdiv, int* hdiv) {
 
 __device__ __forceinline__ int round_u8(float f) { return min(max(__float2int_rn(f), 0), 255); }
 
+#if USV_PREP_FAST
+// Branchless HSV2BGR (the same float operations and the same selected taps as OpenCV's HSV2RGB_f, so
+// bit-identical): a wave holds all six sectors on real frames, and the switch / s == 0 branches ran as
+// divergent paths.  With s == 0 every tap equals v exactly (v * (1 - 0 * x) == v), so that branch
+// needs no special case; H8 <= 255 puts h in [0, 8.5], so the wrap is one conditional subtraction.
+__device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int& og, int& orr) {
+    float h = (float)H8 * (6.f / 180), s = S8 * (1.f / 255.f), v = V8 * (1.f / 255.f);
+    h = h >= 6 ? h - 6 : h;
+    int sector = (int)floorf(h);
+    h -= sector;
+    const bool bad = (unsigned)sector >= 6u;
+    sector = bad ? 0 : sector;
+    h = bad ? 0.f : h;
+    const float t0 = v, t1 = v * (1.f - s), t2 = v * (1.f - s * h), t3 = v * (1.f - s * (1.f - h));
+    // sector_data {1,3,0} {1,0,2} {3,0,1} {0,2,1} {0,1,3} {2,1,0} -> (b, g, r) taps
+    const float b = sector <= 1 ? t1 : sector == 2 ? t3 : sector <= 4 ? t0 : t2;
+    const float g = sector == 0 ? t3 : sector <= 2 ? t0 : sector == 3 ? t2 : t1;
+    const float r = sector == 0 ? t0 : sector == 1 ? t2 : sector <= 3 ? t1 : sector == 4 ? t3 : t0;
+    ob = round_u8(b * 255.f);
+    og = round_u8(g * 255.f);
+    orr = round_u8(r * 255.f);
+}
+#else
 __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int& og, int& orr) {
     float h = (float)H8, s = S8 * (1.f / 255.f), v = V8 * (1.f / 255.f);
     float b, g, r;
@@ -59,10 +86,15 @@ __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int&
     } else {
         const float hscale = 6.f / 180;
         h *= hscale;
+#if USV_PREP_FAST
+        // H8 is a byte: h in [0, 8.5], so OpenCV's wrap loops run at most one subtraction
+        if (h >= 6) h -= 6;
+#else
         if (h < 0)
             do h += 6; while (h < 0);
         else if (h >= 6)
             do h -= 6; while (h >= 6);
+#endif
         int sector = (int)floorf(h);
         h -= sector;
         if ((unsigned)sector >= 6u) {
@@ -84,6 +116,7 @@ __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int&
     og = round_u8(g * 255.f);
     orr = round_u8(r * 255.f);
 }
+#endif
 
 // Work buffer (include/usv.h USV_FRAME_PREP_WORK_BYTES): per parity (the
 // caller alternates it between frames) kHistCopies 256-bin histograms; block
@@ -171,7 +204,8 @@ __global__ __launch_bounds__(256) void hsv_hist_kernel(const uint8_t* __restrict
     __shared__ int sdiv[256], hdiv[256];
     __shared__ uint32_t lh[256];
     const int t = threadIdx.x;
-    hsv_tables(sdiv, hdiv);
+    if (USV_PREP_EXP & 16) { sdiv[t] = 16 * t; hdiv[t] = 7 * t; }  // timing experiment: no per-block table build
+    else hsv_tables(sdiv, hdiv);
     lh[t] = 0;
     if (blockIdx.x == 0)
         for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
@@ -212,6 +246,25 @@ __global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restric
     int hv = 0;
 #pragma unroll
     for (int c = 0; c < kHistCopies; ++c) hv += (int)work[kWHist + kParityWords * parity + 256 * c + t];
+#if USV_PREP_FAST
+    // inclusive scan of the 256 bins: within each wave by shuffles, then the waves' totals
+    __shared__ int wsum[4], wfirst[4];
+    const int lane = t & 63, wv = t >> 6;
+    int x = hv;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    const unsigned long long nz = __ballot(hv != 0);
+    if (lane == 63) wsum[wv] = x;
+    if (lane == 0) wfirst[wv] = nz ? 64 * wv + __ffsll((long long)nz) - 1 : 256;
+    __syncthreads();
+    for (int k = 0; k < wv; ++k) x += wsum[k];
+    scan[t] = x;
+    if (t == 0) first = min(min(wfirst[0], wfirst[1]), min(wfirst[2], wfirst[3]));
+    __syncthreads();
+#else
     if (t == 0) first = 256;
     scan[t] = hv;
     __syncthreads();
@@ -222,6 +275,7 @@ __global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restric
         scan[t] += add;
         __syncthreads();
     }
+#endif
     const int total = W * H, i0 = first;
     int lv = 0;
     if (i0 < 256) {
@@ -234,7 +288,7 @@ __global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restric
             lv = min(max(__float2int_rn(acc * scale), 0), 255);
         }
     }
-    lut[t] = (uint8_t)lv;
+    lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept, result unused)
     __syncthreads();
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
@@ -247,7 +301,8 @@ __global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restric
             for (int k = 0; k < 4; ++k) {
                 in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
                 int b, g, r;
-                hsv2bgr_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], b, g, r);
+                if (USV_PREP_EXP & 8) b = g = r = in.c[3 * k + 2];  // timing experiment: no HSV2BGR
+                else hsv2bgr_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], b, g, r);
                 o.c[3 * k] = b;
                 o.c[3 * k + 1] = g;
                 o.c[3 * k + 2] = r;
