@@ -1311,7 +1311,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     // hold up fewer of the next rows' counted DMA waits.  Needs 4-byte aligned disparity rows.
     const bool wide = USV_WIDE_FLUSH && ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
     auto flush = [&](int rows) {
-        if constexpr (NW > 1) lds_barrier();
+        if constexpr (NW > 1 && USV_PEXP != 12) lds_barrier();  // 12: timing experiment, no barrier (racy)
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
