@@ -1600,8 +1600,11 @@ int resident_pair_blocks_per_cu() {
 // Generation weights of the paired kernel (one-wave workgroups, three generations per SIMD):
 // interleaved A/B on config C, 100:90:70 / 100:80:58 / 100:85:55 / 100:80:50 / 100:75:50 /
 // 100:70:45 = 69.75 / 68.61 / 67.63 / 67.42 / 67.27 / 68.25 us (profiles/probes_r02/ab_pair_weights_*).
+// Re-fitted after the argmin was pipelined into the next row's chain (two A/B runs on two boxes, 4 rounds
+// each): 100:75:50 65.3 / 65.0, 100:70:45 64.4 / 64.7, 100:70:40 64.6, 100:65:40 66.3, 100:60:35 68.5,
+// 100:80:55 66.2, 100:85:60 66.6 us (profiles/probes_r02/ab_pair_weights_3_r02.txt).
 #ifndef USV_PAIR_GEN_WEIGHTS
-#define USV_PAIR_GEN_WEIGHTS 0x32324B64u  // 100, 75, 50, 50
+#define USV_PAIR_GEN_WEIGHTS 0x2D2D4664u  // 100, 70, 45, 45
 #endif
 
 template <int RAD, int NW>
