@@ -1603,8 +1603,12 @@ int resident_pair_blocks_per_cu() {
 // Re-fitted after the argmin was pipelined into the next row's chain (two A/B runs on two boxes, 4 rounds
 // each): 100:75:50 65.3 / 65.0, 100:70:45 64.4 / 64.7, 100:70:40 64.6, 100:65:40 66.3, 100:60:35 68.5,
 // 100:80:55 66.2, 100:85:60 66.6 us (profiles/probes_r02/ab_pair_weights_3_r02.txt).
+// Config E (r = 7, argmin not pipelined) keeps 100:75:50: 617.0 vs 639.9 us with 100:70:45 (same A/B run).
 #ifndef USV_PAIR_GEN_WEIGHTS
-#define USV_PAIR_GEN_WEIGHTS 0x2D2D4664u  // 100, 70, 45, 45
+#define USV_PAIR_GEN_WEIGHTS 0x2D2D4664u  // 100, 70, 45, 45: pipelined argmin (r = 5)
+#endif
+#ifndef USV_PAIR_GEN_WEIGHTS_UNPIPED
+#define USV_PAIR_GEN_WEIGHTS_UNPIPED 0x32324B64u  // 100, 75, 50, 50: r = 6, 7
 #endif
 
 template <int RAD, int NW>
@@ -1628,7 +1632,7 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
     const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
-    P.weights = three ? USV_PAIR_GEN_WEIGHTS : 0x01010101u;
+    P.weights = !three ? 0x01010101u : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
