@@ -1608,7 +1608,14 @@ int resident_pair_blocks_per_cu() {
 #define USV_PAIR_GEN_WEIGHTS 0x2D2D4664u  // 100, 70, 45, 45: pipelined argmin (r = 5)
 #endif
 #ifndef USV_PAIR_GEN_WEIGHTS_UNPIPED
-#define USV_PAIR_GEN_WEIGHTS_UNPIPED 0x32324B64u  // 100, 75, 50, 50: r = 6, 7
+#define USV_PAIR_GEN_WEIGHTS_UNPIPED 0x32324B64u  // 100, 75, 50, 50: r = 6, 7 with one-wave workgroups
+#endif
+// Two-wave workgroups (D > 128: config E) want flatter heights (three interleaved A/B runs of 3 rounds on
+// config E): 100:75:50 620-625, 100:65:40 684, 100:80:60 570, 100:85:60 568, 100:85:65 553-555,
+// 100:85:70 555, 100:90:70 557, 100:90:80 565, 100:95:85 570, uniform 573 us
+// (profiles/probes_r02/ab_pair_weights_E_r02.txt).
+#ifndef USV_PAIR_GEN_WEIGHTS_NW2
+#define USV_PAIR_GEN_WEIGHTS_NW2 0x41415564u  // 100, 85, 65, 65
 #endif
 
 template <int RAD, int NW>
@@ -1632,7 +1639,9 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
     const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
-    P.weights = !three ? 0x01010101u : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
+    P.weights = !three ? 0x01010101u
+              : NW > 1 ? USV_PAIR_GEN_WEIGHTS_NW2
+              : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
