@@ -1636,7 +1636,10 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
                a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
-    P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
+#ifndef USV_PAIR_GEN_G_X4
+#define USV_PAIR_GEN_G_X4 4  // experiment knob: generation size x4/4 (4 = one generation per SIMD-wave slot)
+#endif
+    P.gen_g = (int)((4L * (cu_count() / 8)) * USV_PAIR_GEN_G_X4 / (4 * NW));
     if (P.gen_g < 1) P.gen_g = 1;
     const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
     P.weights = !three ? 0x01010101u
