@@ -67,11 +67,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--extra-steps", type=int, default=20,
                    help="timed frames per extra leg (end-to-end, frame chain, generic fallbacks); 0 = skip")
-    p.add_argument("--event-mode", choices=["sampled", "region", "per-step"], default="sampled",
-                   help="kernel duration from HIP events around every --event-every-th launch of the timed "
-                        "region (default), around every launch (adds ~6 us of wall time per step: each event "
-                        "pair serialises the stream), or the region span / steps")
-    p.add_argument("--event-every", type=int, default=8, help="upper bound; at most steps/8 (>= 8 samples)")
+    p.add_argument("--kernel-steps", type=int, default=50,
+                   help="launches of the separate back-to-back pass after the timed region that gives "
+                        "kernel_ms (HIP events around the pass only, a spin kernel ahead so the host enqueues "
+                        "them all); 0 = use the timed region's span")
     p.add_argument("--pipeline-steps", type=int, default=50,
                    help="timed launches per pipeline leg (rectify / frame prep / mask); 0 = skip")
     return p.parse_args()
@@ -507,16 +506,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    # sampled: every k-th launch, k <= steps / 8 so that short runs (the driver's --steps 20) still time
-    # >= 8 launches (each sampled pair of events costs a few us of wall time, so not every launch)
-    every = 1 if a.event_mode == "per-step" else max(1, min(a.event_every, a.steps // 8))
-    timed = [i for i in range(a.steps) if i % every == every // 2] if a.event_mode != "region" else []
-    events = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed}
+    # The timed region carries no per-launch events (each event pair serialises the stream and costs
+    # ~6 us of wall time, profiles/probes/launch_overhead_r01.txt): one event pair brackets the whole
+    # region on the kernel's stream (span), and the per-launch kernel time comes from a separate
+    # back-to-back pass after it (kernel_ms).
     span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
     span[0].record(stream)
     for i in range(a.steps):
-        step(i, events.get(i))
+        step(i)
     span[1].record(stream)
     for b in range(nbuf):
         if pending[b] is not None:
@@ -527,7 +525,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     span_ms = span[0].elapsed_time(span[1]) / a.steps
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in events.values()])) if events else span_ms
+    if a.kernel_steps > 0:
+        kern_ms = time_launches(lambda: matcher.compute(Lt, Rt, with_distance=with_dist,
+                                                        out_disp=disp_bufs[0][0, :rows],
+                                                        out_dist=dist_bufs[0] if with_dist else None),
+                                a.kernel_steps, stream) / 1e3
+    else:
+        kern_ms = span_ms
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -567,15 +571,14 @@ def main():
         },
         "disparity_evals_per_s": value * D,
         "kernel_ms": kern_ms,
-        "kernel_timing": ({"sampled": f"HIP events around every {every}th launch of the timed region "
-                                      f"({len(events)} launches), kernel's stream",
-                           "per-step": "HIP events around every launch of the timed region, kernel's stream",
-                           "region": "HIP events around the timed region on the kernel's stream, span / steps"}
-                          [a.event_mode]),
+        "kernel_timing": (f"HIP events around {a.kernel_steps} back-to-back launches after the timed region "
+                          "(a spin kernel holds the stream while the host enqueues them), kernel's stream"
+                          if a.kernel_steps > 0 else "HIP events around the timed region, span / steps"),
         "span_ms_per_step": span_ms,
         "roofline": {
             "bound": "hbm",
             "achieved": achieved_gbs,
+            "achieved_timed_region": alg_bytes / (span_ms * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
