@@ -270,11 +270,57 @@ def plumbing_rehearsal(a, world: int, rank: int) -> None:
 
 
 def e2e_leg(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
-    """PCIe-inclusive frame time: pinned host pair -> device, match + distance map, u8 disparity
-    and f64 distance back to pinned host memory, one stream, synchronised per frame (the
-    reference's caller hands over host cv::Mat frames).  Never the headline value."""
-    matcher = StereoBlockMatcher(D, w)
+    """PCIe-inclusive frame rate through the streaming engine (usv_frame_stream_*, csrc/usv_stream.hip):
+    host pair in pinned staging -> H2D -> match -> u8 disparity D2H, `depth` frames in flight so the
+    copies of neighbouring frames overlap the kernel (the reference's caller hands over host frames,
+    P/Main.cpp:876-921).  Beside it the serialised per-frame form (one stream, synchronised per frame,
+    f64 distance map shipped back) that round 2 reported.  Never the headline value."""
+    from unsynchronized_stereo_vision_proj325_amd.streaming import FrameStream, expand_distance
+
     H, W = L.shape
+    out = {}
+    for depth in (2, 3, 4):
+        fs = FrameStream(W, H, D, w, depth=depth)
+        # frames already in each slot's pinned staging (a camera driver would DMA them there)
+        staged = []
+        for _ in range(depth):
+            sl, sr = fs.next_inputs()
+            sl[:] = L
+            sr[:] = R
+            t = fs.submit(sl, sr)
+            staged.append(t)
+        for t in staged:
+            fs.wait(t)
+            fs.release(t)
+
+        def run(n):
+            pending = []
+            for _ in range(n):
+                if len(pending) == depth:
+                    t = pending.pop(0)
+                    fs.wait(t)
+                    fs.release(t)
+                sl, sr = fs.next_inputs()
+                pending.append(fs.submit(sl, sr))
+            for t in pending:
+                fs.wait(t)
+                fs.release(t)
+
+        run(2 * depth)
+        t0 = time.perf_counter()
+        run(steps)
+        dt = (time.perf_counter() - t0) / steps
+        out[f"depth{depth}"] = {"ms_per_frame": dt * 1e3, "value": W * H / dt}
+        fs.close()
+    best = min(out, key=lambda k: out[k]["ms_per_frame"])
+    disp = np.zeros((H, W), np.uint8)
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        expand_distance(disp, threads=16)
+    expand_ms = (time.perf_counter() - t0) / reps * 1e3
+
+    matcher = StereoBlockMatcher(D, w)
     hl, hr = torch.from_numpy(L).pin_memory(), torch.from_numpy(R).pin_memory()
     dl, dr = torch.empty((H, W), dtype=torch.uint8, device=dev), torch.empty((H, W), dtype=torch.uint8, device=dev)
     hd = torch.empty((H, W), dtype=torch.uint8).pin_memory()
@@ -294,11 +340,15 @@ def e2e_leg(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> di
     t0 = time.perf_counter()
     for _ in range(steps):
         frame()
-    dt = (time.perf_counter() - t0) / steps
-    return {"ms_per_frame": dt * 1e3, "value": W * H / dt, "unit": "disparity-pixels/s",
-            "bytes_h2d": 2 * W * H, "bytes_d2h": 9 * W * H,
-            "note": "H2D (L, R) + fused matcher + D2H (u8 disparity, f64 distance), pinned host buffers, "
-                    "one stream, synchronised per frame; PCIe-inclusive, not the headline"}
+    ser = (time.perf_counter() - t0) / steps
+    return {"ms_per_frame": out[best]["ms_per_frame"], "value": out[best]["value"], "unit": "disparity-pixels/s",
+            "depth": int(best[5:]), "by_depth": out, "bytes_h2d": 2 * W * H, "bytes_d2h": W * H,
+            "host_distance_expand_ms_16_threads": expand_ms,
+            "serial_fused_f64": {"ms_per_frame": ser * 1e3, "value": W * H / ser, "bytes_d2h": 9 * W * H,
+                                 "note": "H2D + fused matcher + D2H of u8 and f64 maps, one stream, "
+                                         "synchronised per frame (round-2 e2e leg)"},
+            "note": "streaming engine: pinned host pair -> H2D -> match -> u8 disparity D2H, frames in flight "
+                    "overlap; PCIe-inclusive, not the headline"}
 
 
 def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:

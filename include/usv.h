@@ -181,6 +181,37 @@ usv_status usv_batch_sharded(usv_sharded_engine* e, const uint8_t* L, const uint
                              size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
                              const double* lut_cm, int with_distance);
 
+/* ---- streaming host frames (the reference's caller hands over HOST frames per camera
+ * thread, P/Main.cpp:876-921, 1238-1242) ----
+ * `depth` (2..8) frames in flight on the current device: each slot owns pinned host staging,
+ * device buffers and a HIP stream, so frame k+1's H2D, frame k's match and frame k-1's D2H
+ * overlap.  Output: the u8 disparity map in pinned host memory (expand distances on the host
+ * with usv_distance_expand_host); flag USV_STREAM_DEVICE_DIST also computes the f64 cm map on
+ * the device (fused) and copies it back (8 B/px more over PCIe).  Not thread-safe: one caller
+ * thread per stream object (one object per camera pair). */
+typedef struct usv_frame_stream usv_frame_stream;
+#define USV_STREAM_DEVICE_DIST 1
+usv_status usv_frame_stream_create(int W, int H, int D, int w, int metric, int depth, int flags,
+                                   usv_frame_stream** out);
+usv_status usv_frame_stream_destroy(usv_frame_stream* s);
+/* Pinned staging of the slot the NEXT submit uses (dense, pitch W): write the frames there and
+ * pass these pointers to submit to skip the host-side copy.  INVALID_ARG while that slot's
+ * previous frame has not been released. */
+usv_status usv_frame_stream_next_inputs(usv_frame_stream* s, uint8_t** L, uint8_t** R);
+/* Enqueue one pair (HOST pointers, row pitch `pitch`); returns at once with *ticket.  Buffers
+ * other than the slot's staging are copied into it first.  INVALID_ARG when `depth` frames are
+ * still held (release the oldest first). */
+usv_status usv_frame_stream_submit(usv_frame_stream* s, const uint8_t* L, const uint8_t* R, int pitch,
+                                   long long* ticket);
+/* Block until frame `ticket` is done; *disp (and *dist_cm with USV_STREAM_DEVICE_DIST, else pass
+ * NULL) point into the slot's pinned host memory, valid until usv_frame_stream_release. */
+usv_status usv_frame_stream_wait(usv_frame_stream* s, long long ticket, const uint8_t** disp,
+                                 const double** dist_cm);
+usv_status usv_frame_stream_release(usv_frame_stream* s, long long ticket);
+/* HOST: out[y*out_pitch + x] = lut[disp[y*disp_pitch + x]] over n_threads host threads (0 = 1). */
+usv_status usv_distance_expand_host(const uint8_t* disp, int W, int H, int disp_pitch, const double* lut,
+                                    double* out, int out_pitch, int n_threads);
+
 /* HOST: lut_out[d] = distance(d) in cm for d = 0..255 (d = 0 -> +inf for model 0). */
 usv_status usv_distance_lut_cm(int model, double* lut_out);
 /* HOST: the same table in mm (north_star's unit): lut_out[d] = 10 * cm(d). */

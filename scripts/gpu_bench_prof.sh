@@ -16,6 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ]; then echo "FAILED rc=$rc in $name: stopping"; exit $rc; fi
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[ -n "$TESTS" ] && step pytest 600 python -u -m pytest $TESTS -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step bench 300 python bench.py $BARGS
 step trace 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra-steps 0
 exit 0

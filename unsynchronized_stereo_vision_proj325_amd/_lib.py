@@ -33,6 +33,7 @@ STATUS_NAMES = {
 METRIC_SAD, METRIC_SSD = 0, 1
 DIST_MOVING_OBJECT, DIST_CANNY = 0, 1
 KERNEL_AUTO, KERNEL_FAST, KERNEL_GENERIC, KERNEL_TILED = 0, 1, 2, 3
+STREAM_DEVICE_DIST = 1
 
 
 class UsvError(RuntimeError):
@@ -81,6 +82,13 @@ SIGNATURES = {
     "usv_sharded_outputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "usv_batch_sharded": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_size_t, c_int, c_void_p, c_void_p,
                                   c_void_p, c_int]),
+    "usv_frame_stream_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "usv_frame_stream_destroy": (c_int, [c_void_p]),
+    "usv_frame_stream_next_inputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "usv_frame_stream_submit": (c_int, [c_void_p, c_void_p, c_void_p, c_int, POINTER(ctypes.c_longlong)]),
+    "usv_frame_stream_wait": (c_int, [c_void_p, ctypes.c_longlong, POINTER(c_void_p), POINTER(c_void_p)]),
+    "usv_frame_stream_release": (c_int, [c_void_p, ctypes.c_longlong]),
+    "usv_distance_expand_host": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int]),
     "usv_distance_lut_cm": (c_int, [c_int, POINTER(c_double)]),
     "usv_distance_lut_mm": (c_int, [c_int, POINTER(c_double)]),
     "usv_disparity_to_distance": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,

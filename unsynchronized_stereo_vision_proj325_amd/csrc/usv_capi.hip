@@ -40,15 +40,32 @@ usv_status resolve_lut(const double* lut, const double** dev_lut) {
     if (!lut) return USV_OK;
     hipPointerAttribute_t attr{};
     hipError_t e = hipPointerGetAttributes(&attr, lut);
-    if (e == hipSuccess && (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged ||
-                            attr.type == hipMemoryTypeUnified)) {
-        return USV_OK;
+    // The host copy below dereferences the pointer, so it is taken only for memory positively
+    // identified as pageable host memory: hipSuccess with hipMemoryTypeUnregistered, or the
+    // invalid-value error older runtimes return for unregistered host pointers.  Anything else the
+    // runtime knows is passed through (device, managed, unified, VMM-mapped device memory) or
+    // refused (a host type without a device alias).
+    bool pageable = false;
+    if (e == hipSuccess) {
+        switch (attr.type) {
+            case hipMemoryTypeUnregistered:
+                pageable = true;
+                break;
+            case hipMemoryTypeHost:
+                if (!attr.devicePointer) return USV_ERR_INVALID_ARG;
+                *dev_lut = static_cast<const double*>(attr.devicePointer);  // pinned / registered host memory
+                return USV_OK;
+            default:
+                return USV_OK;  // device-accessible as is
+        }
+    } else if (e == hipErrorInvalidValue) {
+        (void)hipGetLastError();  // the failed query left its error behind; clear only that one
+        pageable = true;
+    } else {
+        (void)hipGetLastError();
+        return USV_ERR_HIP;
     }
-    if (e == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer) {
-        *dev_lut = static_cast<const double*>(attr.devicePointer);  // pinned / registered host memory
-        return USV_OK;
-    }
-    (void)hipGetLastError();  // an unregistered pointer may leave an error behind; clear it
+    if (!pageable) return USV_ERR_INVALID_ARG;
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return USV_ERR_HIP;
     std::lock_guard<std::mutex> lock(g_tables_mu);
@@ -123,7 +140,7 @@ usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
 
 extern "C" {
 
-const char* usv_version(void) { return "usv-mi355x 0.1.0 (gfx950)"; }
+const char* usv_version(void) { return "usv-mi355x 0.3.0 (gfx950)"; }
 
 usv_status usv_device_check(int* n_devices) {
     int n = 0;

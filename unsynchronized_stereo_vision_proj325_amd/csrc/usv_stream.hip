@@ -1,0 +1,235 @@
+// usv_stream.hip -- streaming host frames through the matcher (include/usv.h,
+// usv_frame_stream_*).
+//
+// The reference's caller owns HOST frames: each camera thread grabs a frame,
+// rectifies and pre-processes it and hands it on (P/Main.cpp:876-921,
+// 1238-1242).  A per-frame blocking call (copy in, match, copy out, sync)
+// serialises the PCIe transfers with the kernel.  This engine keeps `depth`
+// frames in flight instead: every slot owns pinned host staging, device
+// buffers and its own HIP stream, so frame k+1's H2D, frame k's match and
+// frame k-1's D2H run at once (the copy engines are separate from the CUs and
+// PCIe is full duplex).  Results are the u8 disparity maps by default: the
+// per-pixel distance is a 256-entry table lookup of the disparity
+// (P/DistanceCalculator.cpp:84), expanded on the host only where a caller asks
+// for it (usv_distance_expand_host), so the link carries 1 B per pixel instead
+// of 9.  USV_STREAM_DEVICE_DIST keeps the f64 map on the device path as well.
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "usv.h"
+#include "usv_kernels.hpp"
+
+struct usv_frame_stream {
+    int W = 0, H = 0, D = 0, w = 0, metric = 0, depth = 0, flags = 0, device = 0;
+    size_t frame = 0;  // W * H
+    struct Slot {
+        uint8_t *hL = nullptr, *hR = nullptr, *hDisp = nullptr;  // pinned host staging
+        double* hDist = nullptr;                                 // pinned (USV_STREAM_DEVICE_DIST)
+        uint8_t *dL = nullptr, *dR = nullptr, *dDisp = nullptr;  // device
+        double* dDist = nullptr;
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        long long ticket = -1;  // frame in this slot, -1 = free
+        bool ready = false;     // its results were waited for
+    };
+    std::vector<Slot> slot;
+    long long next = 0;      // ticket of the next submit
+    double* lut = nullptr;   // device distance table (USV_STREAM_DEVICE_DIST)
+};
+
+namespace {
+
+void free_slot(usv_frame_stream::Slot& s) {
+    (void)hipHostFree(s.hL);
+    (void)hipHostFree(s.hR);
+    (void)hipHostFree(s.hDisp);
+    (void)hipHostFree(s.hDist);
+    (void)hipFree(s.dL);
+    (void)hipFree(s.dR);
+    (void)hipFree(s.dDisp);
+    (void)hipFree(s.dDist);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+}
+
+void release(usv_frame_stream* e) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(e->device);
+    for (auto& s : e->slot) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        free_slot(s);
+    }
+    (void)hipFree(e->lut);
+    (void)hipSetDevice(cur);
+    delete e;
+}
+
+usv_frame_stream::Slot* find(usv_frame_stream* e, long long ticket) {
+    if (ticket < 0) return nullptr;
+    auto& s = e->slot[(size_t)(ticket % e->depth)];
+    return s.ticket == ticket ? &s : nullptr;
+}
+
+// Restores the caller's current device on every exit path.
+struct DeviceGuard {
+    int prev = 0;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        ok = hipGetDevice(&prev) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+}  // namespace
+
+extern "C" {
+
+usv_status usv_frame_stream_create(int W, int H, int D, int w, int metric, int depth, int flags,
+                                   usv_frame_stream** out) {
+    if (!out) return USV_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (W <= 0 || H <= 0 || depth < 2 || depth > 8 || (flags & ~USV_STREAM_DEVICE_DIST)) return USV_ERR_INVALID_ARG;
+    if (D < 1 || D > 256 || w < 1 || w > 63 || (w & 1) == 0) return USV_ERR_UNSUPPORTED;
+    if (metric != USV_METRIC_SAD && metric != USV_METRIC_SSD) return USV_ERR_UNSUPPORTED;
+    auto* e = new usv_frame_stream;
+    if (hipGetDevice(&e->device) != hipSuccess) {
+        delete e;
+        return USV_ERR_NO_DEVICE;
+    }
+    e->W = W; e->H = H; e->D = D; e->w = w; e->metric = metric; e->depth = depth; e->flags = flags;
+    e->frame = (size_t)W * H;
+    e->slot.resize((size_t)depth);
+    const bool dd = flags & USV_STREAM_DEVICE_DIST;
+    for (auto& s : e->slot) {
+        if (hipHostMalloc(&s.hL, e->frame, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&s.hR, e->frame, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&s.hDisp, e->frame, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(&s.dL, e->frame) != hipSuccess || hipMalloc(&s.dR, e->frame) != hipSuccess ||
+            hipMalloc(&s.dDisp, e->frame) != hipSuccess ||
+            (dd && (hipHostMalloc(&s.hDist, e->frame * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+                    hipMalloc(&s.dDist, e->frame * sizeof(double)) != hipSuccess)) ||
+            hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            release(e);
+            return USV_ERR_HIP;
+        }
+    }
+    if (dd) {
+        double lut[256];
+        usv_distance_lut_cm(USV_DIST_MOVING_OBJECT, lut);
+        if (hipMalloc(&e->lut, sizeof(lut)) != hipSuccess ||
+            hipMemcpy(e->lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess) {
+            release(e);
+            return USV_ERR_HIP;
+        }
+    }
+    *out = e;
+    return USV_OK;
+}
+
+usv_status usv_frame_stream_destroy(usv_frame_stream* e) {
+    if (!e) return USV_ERR_INVALID_ARG;
+    release(e);
+    return USV_OK;
+}
+
+usv_status usv_frame_stream_next_inputs(usv_frame_stream* e, uint8_t** L, uint8_t** R) {
+    if (!e || !L || !R) return USV_ERR_INVALID_ARG;
+    auto& s = e->slot[(size_t)(e->next % e->depth)];
+    if (s.ticket >= 0) return USV_ERR_INVALID_ARG;  // the slot's previous frame was not collected yet
+    *L = s.hL;
+    *R = s.hR;
+    return USV_OK;
+}
+
+usv_status usv_frame_stream_submit(usv_frame_stream* e, const uint8_t* L, const uint8_t* R, int pitch,
+                                   long long* ticket) {
+    if (!e || !L || !R || !ticket || pitch < e->W) return USV_ERR_INVALID_ARG;
+    auto& s = e->slot[(size_t)(e->next % e->depth)];
+    if ((L == s.hL || R == s.hR) && pitch != e->W) return USV_ERR_INVALID_ARG;  // the staging is dense
+    if (s.ticket >= 0) return USV_ERR_INVALID_ARG;  // depth frames in flight: collect the oldest first
+    DeviceGuard g(e->device);
+    if (!g.ok) return USV_ERR_HIP;
+    const size_t W = (size_t)e->W, H = (size_t)e->H;
+    // Inputs: the slot's own pinned staging (zero-copy, usv_frame_stream_next_inputs) go straight to
+    // the copy engine; any other host buffer is packed into the staging first (a host memcpy).
+    auto stage = [&](const uint8_t* src, uint8_t* pinned) {
+        if (src == pinned) return;
+        for (size_t y = 0; y < H; ++y) std::memcpy(pinned + y * W, src + y * (size_t)pitch, W);
+    };
+    stage(L, s.hL);
+    stage(R, s.hR);
+    if (hipMemcpyAsync(s.dL, s.hL, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess)
+        return USV_ERR_HIP;
+    const bool dd = e->flags & USV_STREAM_DEVICE_DIST;
+    usv_status st = usv_sad_disparity_ex(s.dL, s.dR, e->W, e->H, e->W, e->D, e->w, e->metric, s.dDisp, e->W,
+                                         dd ? s.dDist : nullptr, e->W, dd ? e->lut : nullptr, USV_KERNEL_AUTO,
+                                         s.stream);
+    if (st != USV_OK) {
+        (void)hipStreamSynchronize(s.stream);  // nothing of this frame may still read the staging
+        return st;
+    }
+    if (hipMemcpyAsync(s.hDisp, s.dDisp, e->frame, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+        (dd && hipMemcpyAsync(s.hDist, s.dDist, e->frame * sizeof(double), hipMemcpyDeviceToHost, s.stream) !=
+                   hipSuccess) ||
+        hipEventRecord(s.done, s.stream) != hipSuccess) {
+        (void)hipStreamSynchronize(s.stream);
+        return USV_ERR_HIP;
+    }
+    s.ticket = e->next++;
+    s.ready = false;
+    *ticket = s.ticket;
+    return USV_OK;
+}
+
+usv_status usv_frame_stream_wait(usv_frame_stream* e, long long ticket, const uint8_t** disp, const double** dist_cm) {
+    if (!e || !disp) return USV_ERR_INVALID_ARG;
+    auto* s = find(e, ticket);
+    if (!s) return USV_ERR_INVALID_ARG;
+    if (dist_cm && !(e->flags & USV_STREAM_DEVICE_DIST)) return USV_ERR_INVALID_ARG;
+    if (!s->ready) {
+        if (hipEventSynchronize(s->done) != hipSuccess) return USV_ERR_HIP;
+        s->ready = true;
+    }
+    *disp = s->hDisp;
+    if (dist_cm) *dist_cm = s->hDist;
+    return USV_OK;
+}
+
+usv_status usv_frame_stream_release(usv_frame_stream* e, long long ticket) {
+    if (!e) return USV_ERR_INVALID_ARG;
+    auto* s = find(e, ticket);
+    if (!s) return USV_ERR_INVALID_ARG;
+    if (!s->ready && hipEventSynchronize(s->done) != hipSuccess) return USV_ERR_HIP;
+    s->ticket = -1;
+    s->ready = false;
+    return USV_OK;
+}
+
+usv_status usv_distance_expand_host(const uint8_t* disp, int W, int H, int disp_pitch, const double* lut,
+                                    double* out, int out_pitch, int n_threads) {
+    if (!disp || !lut || !out || W <= 0 || H <= 0 || disp_pitch < W || out_pitch < W || n_threads < 0)
+        return USV_ERR_INVALID_ARG;
+    const int nt = std::max(1, std::min(n_threads == 0 ? 1 : n_threads, H));
+    auto rows = [&](int y0, int y1) {
+        for (int y = y0; y < y1; ++y) {
+            const uint8_t* d = disp + (size_t)y * disp_pitch;
+            double* o = out + (size_t)y * out_pitch;
+            for (int x = 0; x < W; ++x) o[x] = lut[d[x]];
+        }
+    };
+    if (nt == 1) {
+        rows(0, H);
+        return USV_OK;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(rows, (int)((long long)H * t / nt), (int)((long long)H * (t + 1) / nt));
+    for (auto& t : th) t.join();
+    return USV_OK;
+}
+
+}  // extern "C"
