@@ -435,6 +435,113 @@ def frame_chain_graph_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> di
             "matches_eager": same}
 
 
+def matcher_leg(dev, n: int = 150, max_pts: int = 120, runs: int = 5) -> dict:
+    """The reference's contour matcher on the host beside the engine's forms:
+    N = M = n blob contours of 12..max_pts points.  Times (median of `runs` after one warm-up, host
+    core count stated): the oracle's GenerateMatchingList, which recomputes both contours' Hu moments
+    and four contourArea calls per pair as P/Main.cpp:403-426 does (the reference's algorithm, single
+    thread); the host restatement (usv_generate_matching_list: descriptors once per contour); the GPU
+    form (GenerateMatchingListGPU: descriptors + N x M scores in two launches, points H2D and scores
+    D2H included); and ResolveMatchList (P/Main.cpp:432-477, the "VERy slow" step of :1079) in the
+    oracle and the host C++.  The lists are checked equal (host bit-exact, GPU scores to 1e-12)."""
+    import ctypes
+    import math
+    import random
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import _flat, load_oracle, oracle_match
+    from unsynchronized_stereo_vision_proj325_amd import _lib
+    from unsynchronized_stereo_vision_proj325_amd.contours import (GenerateMatchingListGPU, contour_descriptors,
+                                                                   contour_pair_scores)
+
+    rng = random.Random(325)
+
+    def blob():
+        cx, cy, r = rng.randint(40, 600), rng.randint(40, 440), rng.randint(8, 60)
+        ang = sorted(rng.uniform(0, 2 * math.pi) for _ in range(rng.randint(12, max_pts)))
+        return [(int(cx + r * rng.uniform(0.7, 1.0) * math.cos(a)), int(cy + r * rng.uniform(0.7, 1.0) * math.sin(a)))
+                for a in ang]
+
+    A, B = [blob() for _ in range(n)], [blob() for _ in range(n)]
+    ora, lib = load_oracle(), _lib.load()
+    pa, oa = _flat(A)
+    pb, ob = _flat(B)
+    cap = n * n
+    o_out = (oracle_match * cap)()
+    h_out = (_lib.usv_match * cap)()
+    nh = ctypes.c_int(0)
+    ip = ctypes.POINTER(ctypes.c_int)
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+
+    n_o = [0]
+
+    def oracle_gml():
+        n_o[0] = ora.usv_oracle_generate_matching_list(pa.ctypes.data, oa.ctypes.data, n, pb.ctypes.data,
+                                                       ob.ctypes.data, n, o_out)
+
+    def host_gml():
+        _lib.check("usv_generate_matching_list", lib.usv_generate_matching_list(
+            pa.ctypes.data_as(ip), oa.ctypes.data_as(ip), n, pb.ctypes.data_as(ip), ob.ctypes.data_as(ip), n,
+            h_out, cap, ctypes.byref(nh)))
+
+    gpu_res = [None]
+
+    def gpu_gml():
+        gpu_res[0] = GenerateMatchingListGPU(A, B, device=dev)
+
+    def gpu_scores():  # descriptors + N x M scores on the device, scores back, threshold scan
+        sc = contour_pair_scores(contour_descriptors(A, dev), contour_descriptors(B, dev)).cpu().numpy()
+        np.nonzero(sc < 0.75)
+
+    t_oracle, t_host, t_gpu, t_gpu_scores = med(oracle_gml), med(host_gml), med(gpu_gml), med(gpu_scores)
+    ref = [(o_out[i].left, o_out[i].right, o_out[i].value) for i in range(n_o[0])]
+    host = [(h_out[i].left_index, h_out[i].right_index, h_out[i].match_value) for i in range(nh.value)]
+    gpu = gpu_res[0]
+    same_host = host == ref
+    same_gpu = len(gpu) == len(ref) and all(g[:2] == r[:2] and abs(g[2] - r[2]) <= 1e-12 * (1 + abs(r[2]))
+                                            for g, r in zip(gpu, ref))
+    m = len(ref)
+    r_in = (oracle_match * max(m, 1))()
+    for i, (l, r, v) in enumerate(ref):
+        r_in[i].left, r_in[i].right, r_in[i].value = l, r, v
+    r_out = (oracle_match * max(m, 1))()
+    h_in = (_lib.usv_match * max(m, 1))()
+    for i, (l, r, v) in enumerate(ref):
+        h_in[i].left_index, h_in[i].right_index, h_in[i].match_value = l, r, v
+    h_res = (_lib.usv_match * max(m, 1))()
+    nr, nrh = [0], ctypes.c_int(0)
+
+    def oracle_rml():
+        nr[0] = ora.usv_oracle_resolve_match_list(r_in, m, r_out)
+
+    def host_rml():
+        _lib.check("usv_resolve_match_list", lib.usv_resolve_match_list(h_in, m, h_res, ctypes.byref(nrh)))
+
+    t_ro, t_rh = med(oracle_rml), med(host_rml)
+    same_rml = nr[0] == nrh.value and all(
+        (r_out[i].left, r_out[i].right, r_out[i].value) == (h_res[i].left_index, h_res[i].right_index,
+                                                             h_res[i].match_value) for i in range(nr[0]))
+    return {"workload": f"N = M = {n} contours of 12..{max_pts} points (seeded blobs), {m} pairs under 0.75",
+            "cores": 1, "runs": runs,
+            "generate_matching_list_ms": {"reference_algorithm_oracle": t_oracle, "host_cpp": t_host,
+                                          "gpu": t_gpu, "gpu_scores_only": t_gpu_scores},
+            "resolve_match_list_ms": {"reference_algorithm_oracle": t_ro, "host_cpp": t_rh},
+            "speedup_host_vs_reference": t_oracle / t_host, "speedup_gpu_vs_reference": t_oracle / t_gpu,
+            "lists_equal": {"host": same_host, "gpu": same_gpu, "resolve": same_rml},
+            "note": "single host thread for the CPU forms; gpu = contours.GenerateMatchingListGPU (point H2D, "
+                    "descriptor + score launches, score D2H, threshold scan, Python list of tuples); gpu_scores_only "
+                    "= the same without building the Python list; resolve host_cpp = indexed form (per-index "
+                    "position lists), same output as the reference's scan"}
+
+
 def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
     """What the AUTO dispatch costs off the fast SAD kernels: the tiled sliding-window kernel
     (csrc/usv_sad_tiled.hip) for SSD at the headline config and for SAD on a 1918-wide (W % 4 != 0)
@@ -660,6 +767,7 @@ def main():
         rec["frame_chain"] = frame_chain_leg(dev, W, H, D, w, a.extra_steps)
         rec["frame_chain_graph"] = frame_chain_graph_leg(dev, W, H, D, w, a.extra_steps)
         rec["fallbacks"] = fallback_legs(dev, L, R, D, w, max(2, a.extra_steps // 4))
+        rec["matcher"] = matcher_leg(dev)
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
         rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]

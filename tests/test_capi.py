@@ -240,3 +240,28 @@ def test_match_layout_matches_reference_build():
     ref.ref_match_construct(7, 4000000000, -0.125, buf)
     ours = _lib.usv_match(7, 4000000000, -0.125)
     assert bytes(buf)[:16] == bytes(ours)[:16]
+
+
+def test_resolve_match_list_large_vs_oracle(oracle):
+    """The indexed ResolveMatchList (per-index position lists) against the oracle's linear scan of
+    P/Main.cpp:432-477 on larger lists: dense and sparse index ranges, value ties, duplicates."""
+    rng = np.random.default_rng(11)
+    for n, nl, nr, ties in [(2000, 40, 40, False), (3000, 12, 300, True), (1500, 1500, 1500, False),
+                            (500, 3, 3, True), (800, 1 << 20, 5, False)]:
+        m = _rand_matches(rng, n, nl, nr)
+        if ties:
+            m = [(l, r, round(v, 2)) for l, r, v in m]
+        got = host.ResolveMatchList(m)
+        arr = (oracle_match * n)()
+        for i, (l, r, v) in enumerate(m):
+            arr[i].left, arr[i].right, arr[i].value = l, r, v
+        out = (oracle_match * n)()
+        k = oracle.usv_oracle_resolve_match_list(arr, n, out)
+        assert got == [(out[i].left, out[i].right, out[i].value) for i in range(k)], (n, nl, nr)
+    big = [(1 << 25, 0, 0.5), (1 << 25, 1, 0.25), (3, 1, 0.1)]  # indices past the dense range: the plain scan
+    arr = (oracle_match * 3)()
+    for i, (l, r, v) in enumerate(big):
+        arr[i].left, arr[i].right, arr[i].value = l, r, v
+    out = (oracle_match * 3)()
+    k = oracle.usv_oracle_resolve_match_list(arr, 3, out)
+    assert host.ResolveMatchList(big) == [(out[i].left, out[i].right, out[i].value) for i in range(k)]

@@ -12,8 +12,10 @@
 // per-pair arithmetic on them is unchanged, so the scores are identical.
 #include "Matching.hpp"
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <vector>
 
 #include "usv.h"
 
@@ -165,17 +167,68 @@ void ResolveMatchList(std::vector<Match> Matcher, std::vector<Match>& TentativeM
     // P/Main.cpp:475).  A candidate replaces every conflicting tentative entry
     // it beats; if it beats none it is appended even when a better conflicting
     // entry exists, so duplicates can appear.
+    //
+    // The reference scans the whole tentative list for every candidate (O(n |T|),
+    // "VERy slow", P/Main.cpp:1079).  Here the entries sharing an index are found
+    // through per-index position lists instead: each entry's decision depends only
+    // on itself and the candidate, so visiting the sharing positions in any order
+    // gives the same list.  Lists are lazy (a replaced entry stays in its old
+    // index's list and is skipped there when its index no longer matches).
     TentativeMatch.clear();
+    if (Matcher.empty()) return;
+    unsigned maxL = 0, maxR = 0;
     for (const Match& m : Matcher) {
-        bool replaced = false;
-        for (Match& t : TentativeMatch) {
-            const bool shares = t.LeftIndex == m.LeftIndex || t.RightIndex == m.RightIndex;
-            if (shares && t.MatchValue > m.MatchValue) {
-                t = m;
-                replaced = true;
+        maxL = std::max(maxL, m.LeftIndex);
+        maxR = std::max(maxR, m.RightIndex);
+    }
+    if (maxL >= (1u << 24) || maxR >= (1u << 24)) {  // sparse indices: the reference's scan
+        for (const Match& m : Matcher) {
+            bool replaced = false;
+            for (Match& t : TentativeMatch) {
+                const bool shares = t.LeftIndex == m.LeftIndex || t.RightIndex == m.RightIndex;
+                if (shares && t.MatchValue > m.MatchValue) {
+                    t = m;
+                    replaced = true;
+                }
             }
+            if (!replaced) TentativeMatch.push_back(m);
         }
-        if (!replaced) TentativeMatch.push_back(m);
+        return;
+    }
+    std::vector<std::vector<unsigned>> byL(maxL + 1), byR(maxR + 1);
+    std::vector<size_t> seen;  // visit stamp per position (a position may sit in both lists)
+    TentativeMatch.reserve(Matcher.size());
+    size_t stamp = 0;
+    for (const Match& m : Matcher) {
+        ++stamp;
+        bool replaced = false;
+        auto visit = [&](std::vector<unsigned>& list, bool left) {
+            // entries appended during this visit (the candidate's own) are past `n`; index access,
+            // since an append may reallocate the list
+            const size_t n = list.size();
+            for (size_t i = 0; i < n; ++i) {
+                const unsigned p = list[i];
+                if (seen[p] == stamp) continue;
+                Match& t = TentativeMatch[p];
+                if ((left ? t.LeftIndex : t.RightIndex) != (left ? m.LeftIndex : m.RightIndex)) continue;  // stale
+                seen[p] = stamp;
+                if (t.MatchValue > m.MatchValue) {
+                    t = m;
+                    replaced = true;
+                    byL[m.LeftIndex].push_back(p);  // may duplicate: the stamp skips the second visit
+                    byR[m.RightIndex].push_back(p);
+                }
+            }
+        };
+        visit(byL[m.LeftIndex], true);
+        visit(byR[m.RightIndex], false);
+        if (!replaced) {
+            const unsigned p = (unsigned)TentativeMatch.size();
+            TentativeMatch.push_back(m);
+            seen.push_back(0);
+            byL[m.LeftIndex].push_back(p);
+            byR[m.RightIndex].push_back(p);
+        }
     }
 }
 
