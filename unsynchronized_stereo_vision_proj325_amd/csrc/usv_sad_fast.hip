@@ -1464,6 +1464,129 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     };
     auto no_pre = [](auto) {};
 
+    // ---- prefetched row boundary (USV_PAIR_PREF, pipelined r = 5 only) ----
+    // Without it every row starts with an s_waitcnt lgkmcnt(0) (the pinned L words are a scalar
+    // load, which returns out of order) that also retires the previous row's transpose reads issued
+    // just before, then issues its staged-entry reads and waits for the first of them: two LDS round
+    // trips per row with nothing else of this wave to issue.  Here the boundary is reordered:
+    //   end of row t:  lgkmcnt(0) (everything of row t, and the L words of row t + 1 loaded a row
+    //                  earlier) -> extract row t + 1's L bytes -> [flush] -> scalar-load row t + 2's
+    //                  L words -> vmcnt wait for row t + 1's DMA -> the first PV vector reads of
+    //                  row t + 1's staged entries -> row t's transpose WRITES;
+    //   row t + 1:     DMA, ring subtraction, the remaining entry reads, THEN the transpose reads,
+    //                  the chain (its first steps run on the prefetched entries) with the argmin
+    //                  pieces from step PIECE_OFF on, so the transpose reads have a whole run of
+    //                  chain steps to land.
+#ifndef USV_PAIR_PREF
+#define USV_PAIR_PREF 0  // vector reads of the next row prefetched (0 = off)
+#endif
+#ifndef USV_PAIR_PIECE_OFF
+#define USV_PAIR_PIECE_OFF 8  // chain step of the first argmin piece (USV_PAIR_PREF)
+#endif
+    constexpr bool PREF = USV_PAIR_PREF > 0 && kPairPipe<RAD> && C::SPLIT == 1;
+    using VTp = typename VecT<C::VEC>::T;
+    constexpr int NVp = C::NE_V / C::VEC;
+    constexpr int PV = PREF ? (USV_PAIR_PREF < NVp ? USV_PAIR_PREF : NVp) : 1;
+    constexpr int OFFP = USV_PAIR_PIECE_OFF;
+    uint32_t Epf[PV * C::VEC];
+    uint32_t Lv[NPOS];  // L bytes of the row about to run
+    auto extract_l = [&]() {  // after wait_lgkm0_pin(lw_next)
+        LWords cur = lw_next;
+        uint32_t lw[8];
+        unpack_words<LS::NLD>(cur, lw);
+#pragma unroll
+        for (int j = 0; j < NPOS; ++j) {
+            const int bidx = LS::byte(j);
+            if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+            else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+        }
+    };
+    auto prefetch_e = [&](int t_next) {
+        wait_vmcnt<(PD - 1) * NDMA>();  // row t_next's DMA (issued PD rows ago) has landed
+        __builtin_amdgcn_wave_barrier();
+        int boff = (t_next & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const VTp v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) Epf[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+    };
+    auto tr_write = [&](const uint32_t(&S)[K]) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        asm volatile("" ::: "memory");
+    };
+    auto tr_read = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) trq[j] = reinterpret_cast<const uint4*>(tb)[rdw[j]];
+        asm volatile("" ::: "memory");
+    };
+    auto do_row_pref = [&](int t_in, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
+        constexpr int I = decltype(i_tag)::value;
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));
+            const int buf = (t + PD) & (NB - 1);
+            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            rawR = rr + a.pitch;
+        }
+#pragma unroll
+        for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        uint32_t E[C::NE_V];
+#pragma unroll
+        for (int e = 0; e < PV * C::VEC; ++e) E[e] = Epf[e];
+        int boff = (t & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
+#pragma unroll
+        for (int k = PV; k < NVp; ++k) {
+            const VTp v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+        tr_read();
+        uint32_t A[NPOS + 1];
+        A[0] = 0;
+        auto chain_step = [&](auto jt) {
+            constexpr int j = decltype(jt)::value;
+            const uint32_t l = Lv[j];
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            if constexpr (j >= OFFP && j - OFFP < 16) tr_piece(std::integral_constant<int, j - OFFP>{}, I);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (chain_step(std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, NPOS>{});
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            ((J >= (NPOS - OFFP > 0 ? NPOS - OFFP : 0) ? tr_piece(std::integral_constant<int, J>{}, I) : void()), ...);
+        }(std::make_integer_sequence<int, 16>{});
+#pragma unroll
+        for (int x = 0; x < K; ++x) {
+            const uint32_t h = A[x + WIN] - A[x];
+            S[x] = S[x] + h;
+            ring[I][x] = h;
+        }
+    };
+    auto row_tail = [&](int t, bool do_flush, const uint32_t(&S)[K]) {
+        wait_lgkm0_pin<LS::NLD>(lw_next);
+        extract_l();
+        if (do_flush) flush(KRB);
+        {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        }
+        prefetch_e(t + 1);
+        tr_write(S);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
     uint32_t S[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
@@ -1482,7 +1605,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     constexpr bool PIPE = kPairPipe<RAD>;
     static_assert(KRB == WIN, "pending slot = row index in the unrolled group");
     static_assert(!PIPE || NPOS >= 16, "16 argmin pieces ride on the chain steps");
-    if constexpr (PIPE) {
+    if constexpr (PREF) {
+        row_tail(WIN - 1, false, S);
+    } else if constexpr (PIPE) {
         tr_issue(S);
         __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -1490,7 +1615,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     }
     auto step = [&](int t0, auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
-        if constexpr (PIPE) {
+        if constexpr (PREF) {
+            do_row_pref(t0 + I, i_tag, S, ring);
+            row_tail(t0 + I, I == KRB - 1, S);
+        } else if constexpr (PIPE) {
             do_row(t0 + I, SteadyT{}, i_tag, S, ring, [&](auto jt) {
                 if constexpr (decltype(jt)::value < 16) tr_piece(jt, I);
             });
@@ -1512,6 +1640,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
     if constexpr (PIPE) {
         const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
+        if constexpr (PREF) tr_read();
         tr_finish(last);
         if (last == KRB - 1) flush(KRB);
     }
