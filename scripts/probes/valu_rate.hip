@@ -52,6 +52,18 @@ PROBE(p_msad_u8, "v_msad_u8 %0, %1, %2, %0")
 PROBE(p_bfe_u32, "v_bfe_u32 %0, %1, 8, 8")
 PROBE(p_max3_u32, "v_max3_u32 %0, %1, %2, %0")
 PROBE(p_pk_mad_u16, "v_pk_mad_u16 %0, %1, %2, %0")
+PROBE(p_sad_u32, "v_sad_u32 %0, %1, %2, %0")
+PROBE(p_sad_u16, "v_sad_u16 %0, %1, %2, %0")
+PROBE(p_add3_u32, "v_add3_u32 %0, %1, %2, %0")
+PROBE(p_sub_u32, "v_sub_u32 %0, %0, %1")
+PROBE(p_or_b32, "v_or_b32 %0, %1, %0")
+PROBE(p_lshl_add, "v_lshl_add_u32 %0, %1, 8, %0")
+PROBE(p_mad_u24, "v_mad_u32_u24 %0, %1, %2, %0")
+PROBE(p_mul_u24, "v_mul_u32_u24 %0, %1, %0")
+PROBE(p_mul_lo, "v_mul_lo_u32 %0, %1, %0")
+PROBE(p_alignbyte, "v_alignbyte_b32 %0, %1, %0, 1")
+PROBE(p_and_or, "v_and_or_b32 %0, %1, %2, %0")
+PROBE(p_xad, "v_xad_u32 %0, %1, %2, %0")
 
 // Mixed streams: cycles per loop iteration (16 VALU [+ 16 or 8 SALU]) per SIMD.
 #define SBODY8                                                                          \
@@ -113,7 +125,13 @@ int main() {
                         {"v_min_u32_dpp", p_mov_dpp},     {"v_permlane32_swap", p_permlane32},
                         {"v_dot4_u32_u8", p_dot4_u8},
                         {"v_msad_u8", p_msad_u8},         {"v_bfe_u32", p_bfe_u32},
-                        {"v_max3_u32", p_max3_u32},       {"v_pk_mad_u16", p_pk_mad_u16}};
+                        {"v_max3_u32", p_max3_u32},       {"v_pk_mad_u16", p_pk_mad_u16},
+                        {"v_sad_u32", p_sad_u32},         {"v_sad_u16", p_sad_u16},
+                        {"v_add3_u32", p_add3_u32},       {"v_sub_u32", p_sub_u32},
+                        {"v_or_b32", p_or_b32},           {"v_lshl_add_u32", p_lshl_add},
+                        {"v_mad_u32_u24", p_mad_u24},     {"v_mul_u32_u24", p_mul_u24},
+                        {"v_mul_lo_u32", p_mul_lo},       {"v_alignbyte_b32", p_alignbyte},
+                        {"v_and_or_b32", p_and_or},       {"v_xad_u32", p_xad}};
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     uint32_t* out;

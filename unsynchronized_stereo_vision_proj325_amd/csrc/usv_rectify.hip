@@ -75,17 +75,37 @@ struct RemapJob {
     int dpitch;
 };
 
-// 4 output pixels per thread: the map arrives as one 16-B and one 8-B load
-// (when the rows are 4-pixel aligned), the four taps of each pixel come from
-// L2 / L1 (a rectification map moves a pixel by a few source columns), the
-// result leaves as one 4-B (gray) or three 4-B (BGR) stores.
+// 4 output pixels (one quad) per thread over a flat range of quads per camera: the map arrives as
+// one 16-B and one 8-B load (when the rows are 4-pixel aligned), the four taps of each pixel come
+// from L2 / L1 (a rectification map moves a pixel by a few source columns), the result leaves as
+// one 4-B (gray) or one 12-B (BGR) store.
+//   * Blocks are numbered XCD-contiguously (block b runs on XCD b % 8, and XCD k takes the k-th
+//     contiguous run of quads), so the source rows one output band reads are fetched into one L2.
+//   * Fixed point: every weight of OpenCV's bilinear table is a multiple of 32 and the four sum to
+//     32768, so (S00 w0 + S01 w1 + S10 w2 + S11 w3 + 2^14) >> 15 = (S00 a0 + ... + 2^9) >> 10 with
+//     a = w / 32 <= 1024: products < 2^18, sums < 2^24 and never above 255 after the shift.  The
+//     two taps of a row are one u16 pair and their weights another, so each channel is two
+//     v_dot2_u32_u16 (full-rate integer ops; the 32-bit multiplies they replace issue at a quarter
+//     of the rate and bounded the round-2 kernel).
+//   * Source offsets are 32-bit (sy * pitch + byte, a 24-bit multiply) from the job's base pointer.
+typedef unsigned short usv_us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(usv_us2, a), __builtin_bit_cast(usv_us2, b), c, false);
+}
+
 template <int CN>
 __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
-                                                    int vec_map, int vec_dst, int vec_src) {
-    const RemapJob& j = blockIdx.z ? j1 : j0;
-    const int y = blockIdx.y;
-    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (x0 >= W || y >= H) return;
+                                                    unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
+    const unsigned total = gridDim.x, lin = blockIdx.x;
+    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
+    const unsigned lb = xcd * base + min(xcd, rem) + (lin >> 3);
+    const unsigned job = lb >= blocks_per_job ? 1u : 0u;
+    const RemapJob& j = job ? j1 : j0;
+    const unsigned nq = (unsigned)(W + 3) >> 2;
+    const unsigned q = (lb - job * blocks_per_job) * 256u + threadIdx.x;
+    if (q >= nq * (unsigned)H) return;
+    const int y = (int)(q / nq);
+    const int x0 = 4 * (int)(q - (unsigned)y * nq);
     const int n = min(4, W - x0);
     const size_t mrow = (size_t)y * W + x0;
     int mx[4], my[4], mf[4];
@@ -94,50 +114,50 @@ __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, in
         const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
         const int w4[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            mx[q] = (int)(int16_t)(w4[q] & 0xFFFF);
-            my[q] = (int)(int16_t)((unsigned)w4[q] >> 16);
+        for (int k = 0; k < 4; ++k) {
+            mx[k] = (int)(int16_t)(w4[k] & 0xFFFF);
+            my[k] = (int)(int16_t)((unsigned)w4[k] >> 16);
         }
         mf[0] = f.x & 0xFFFF;
         mf[1] = f.x >> 16;
         mf[2] = f.y & 0xFFFF;
         mf[3] = f.y >> 16;
     } else {
-        for (int q = 0; q < 4; ++q) {
-            const int qq = q < n ? q : 0;
-            mx[q] = j.map1[2 * (mrow + qq)];
-            my[q] = j.map1[2 * (mrow + qq) + 1];
-            mf[q] = j.map2[mrow + qq];
+        for (int k = 0; k < 4; ++k) {
+            const int kk = k < n ? k : 0;
+            mx[k] = j.map1[2 * (mrow + kk)];
+            my[k] = j.map1[2 * (mrow + kk) + 1];
+            mf[k] = j.map2[mrow + kk];
         }
     }
-    uint8_t out[4 * CN];
+    uint32_t out[4 * CN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int sx = mx[q], sy = my[q];
-        const int ty = mf[q] >> 5, tx = mf[q] & 31;
-        const int w0 = (32 - ty) * (32 - tx) * 32, w1 = (32 - ty) * tx * 32;
-        const int w2 = ty * (32 - tx) * 32, w3 = ty * tx * 32;
+    for (int k = 0; k < 4; ++k) {
+        const int sx = mx[k], sy = my[k];
+        const uint32_t ty = (uint32_t)mf[k] >> 5, tx = (uint32_t)mf[k] & 31u;
+        // row weights as u16 pairs: (32 - tx, tx) scaled by (32 - ty) for row 0, by ty for row 1
+        const uint32_t wx = (32u - tx) | (tx << 16);
+        const uint32_t wr0 = wx * (32u - ty), wr1 = wx * ty;  // both halves <= 1024: no carry
         if (sx >= sW || sx + 1 < 0 || sy >= sH || sy + 1 < 0) {
 #pragma unroll
-            for (int k = 0; k < CN; ++k) out[q * CN + k] = 0;
+            for (int c = 0; c < CN; ++c) out[k * CN + c] = 0;
             continue;
         }
         const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
-        const uint8_t* r0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
-        const uint8_t* r1 = r0 + j.spitch;
-        // Interior: both taps of a row are 2*CN adjacent bytes; read the aligned
-        // dwords that hold them (2 for gray, 3 for BGR) and funnel-shift, unless
-        // the aligned read could run past the last source row.
-        constexpr int NW = CN == 1 ? 2 : 3;
+        // Interior: both taps of a row are 2*CN adjacent bytes; read the aligned dwords that hold
+        // them (2 for gray, 3 for BGR) and funnel-shift, unless the aligned read could run past
+        // the last source row.
+        constexpr int NWD = CN == 1 ? 2 : 3;
         const int boff = sx * CN, a = boff & ~3, o = boff & 3;
         const bool interior = x0ok && x1ok && y0ok && y1ok && vec_src &&
-                              (sy + 1 < sH - 1 || a + 4 * NW <= j.spitch);
+                              (sy + 1 < sH - 1 || a + 4 * NWD <= j.spitch);
         if (interior) {
-            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + (ptrdiff_t)sy * j.spitch + a);
-            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(q0) + j.spitch);
-            uint32_t u0[NW], u1[NW];
+            const uint32_t r0 = __umul24((uint32_t)sy, (uint32_t)j.spitch) + (uint32_t)a;  // both < 2^24 (launch)
+            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
+            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r0 + (uint32_t)j.spitch);
+            uint32_t u0[NWD], u1[NWD];
 #pragma unroll
-            for (int i = 0; i < NW; ++i) {
+            for (int i = 0; i < NWD; ++i) {
                 u0[i] = q0[i];
                 u1[i] = q1[i];
             }
@@ -149,34 +169,41 @@ __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, in
                 h1 = __builtin_amdgcn_alignbyte(u1[2], u1[1], o);
             }
 #pragma unroll
-            for (int k = 0; k < CN; ++k) {
-                const int kb = CN + k;  // byte of the right tap
-                const int v0 = (l0 >> (8 * k)) & 0xFF, v2 = (l1 >> (8 * k)) & 0xFF;
-                const int v1 = kb < 4 ? (l0 >> (8 * kb)) & 0xFF : (h0 >> (8 * (kb - 4))) & 0xFF;
-                const int v3 = kb < 4 ? (l1 >> (8 * kb)) & 0xFF : (h1 >> (8 * (kb - 4))) & 0xFF;
-                const int t = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
-                out[q * CN + k] = (uint8_t)min(t, 255);
+            for (int c = 0; c < CN; ++c) {
+                // (left tap | right tap << 16) of each row: byte c and byte CN + c of (h:l)
+                const int kb = CN + c;
+                const uint32_t sel = 0x0c000c00u | (uint32_t)(4 + c) | ((uint32_t)(kb < 4 ? 4 + kb : kb - 4) << 16);
+                const uint32_t p0 = __builtin_amdgcn_perm(kb < 4 ? l0 : h0, l0, sel);
+                const uint32_t p1 = __builtin_amdgcn_perm(kb < 4 ? l1 : h1, l1, sel);
+                out[k * CN + c] = dot2(p0, wr0, dot2(p1, wr1, 1u << 9)) >> 10;
             }
             continue;
         }
+        const uint8_t* rp0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
+        const uint8_t* rp1 = rp0 + j.spitch;
+        const uint32_t w0 = wr0 & 0xFFFFu, w1 = wr0 >> 16, w2 = wr1 & 0xFFFFu, w3 = wr1 >> 16;
 #pragma unroll
-        for (int k = 0; k < CN; ++k) {
-            const int v0 = (x0ok && y0ok) ? r0[k] : 0;
-            const int v1 = (x1ok && y0ok) ? r0[CN + k] : 0;
-            const int v2 = (x0ok && y1ok) ? r1[k] : 0;
-            const int v3 = (x1ok && y1ok) ? r1[CN + k] : 0;
-            const int t = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
-            out[q * CN + k] = (uint8_t)min(max(t, 0), 255);
+        for (int c = 0; c < CN; ++c) {
+            const uint32_t v0 = (x0ok && y0ok) ? rp0[c] : 0;
+            const uint32_t v1 = (x1ok && y0ok) ? rp0[CN + c] : 0;
+            const uint32_t v2 = (x0ok && y1ok) ? rp1[c] : 0;
+            const uint32_t v3 = (x1ok && y1ok) ? rp1[CN + c] : 0;
+            out[k * CN + c] = (__umul24(v0, w0) + __umul24(v1, w1) + __umul24(v2, w2) + __umul24(v3, w3) + (1u << 9)) >> 10;
         }
     }
     uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
     if (vec_dst && n == 4) {
-#pragma unroll
-        for (int w = 0; w < CN; ++w)
-            reinterpret_cast<uint32_t*>(d)[w] = (uint32_t)out[4 * w] | ((uint32_t)out[4 * w + 1] << 8) |
-                                                ((uint32_t)out[4 * w + 2] << 16) | ((uint32_t)out[4 * w + 3] << 24);
+        if constexpr (CN == 3) {
+            uint3 w;
+            w.x = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+            w.y = out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24);
+            w.z = out[8] | (out[9] << 8) | (out[10] << 16) | (out[11] << 24);
+            *reinterpret_cast<uint3*>(d) = w;
+        } else {
+            *reinterpret_cast<uint32_t*>(d) = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+        }
     } else {
-        for (int b = 0; b < n * CN; ++b) d[b] = out[b];
+        for (int b = 0; b < n * CN; ++b) d[b] = (uint8_t)out[b];
     }
 }
 
@@ -191,11 +218,20 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
         vec_dst = vec_dst && aligned(j.dst, 4) && (j.dpitch % 4) == 0;
         vec_src = vec_src && aligned(j.src, 4) && (j.spitch % 4) == 0;
     }
-    dim3 grid((unsigned)((W + 1023) / 1024), (unsigned)H, (unsigned)n_jobs), block(256);
+    // 32-bit source offsets: sy * spitch + byte stays below 2^32
+    if ((long long)(sH + 1) * a.spitch >= (1LL << 32) || (long long)(sH + 1) * b.spitch >= (1LL << 32) ||
+        a.spitch >= (1 << 24) || b.spitch >= (1 << 24))
+        return USV_ERR_UNSUPPORTED;
+    const long long quads = (long long)((W + 3) / 4) * H;
+    const long long per_job = (quads + 255) / 256;
+    if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
+    dim3 grid((unsigned)(per_job * n_jobs)), block(256);
     if (cn == 1)
-        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst, (int)vec_src);
+        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map,
+                           (int)vec_dst, (int)vec_src);
     else if (cn == 3)
-        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (int)vec_map, (int)vec_dst, (int)vec_src);
+        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map,
+                           (int)vec_dst, (int)vec_src);
     else
         return USV_ERR_UNSUPPORTED;
     return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
