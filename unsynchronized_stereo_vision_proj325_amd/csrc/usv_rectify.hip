@@ -172,9 +172,10 @@ __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, in
             for (int c = 0; c < CN; ++c) {
                 // (left tap | right tap << 16) of each row: byte c and byte CN + c of (h:l)
                 const int kb = CN + c;
-                const uint32_t sel = 0x0c000c00u | (uint32_t)(4 + c) | ((uint32_t)(kb < 4 ? 4 + kb : kb - 4) << 16);
-                const uint32_t p0 = __builtin_amdgcn_perm(kb < 4 ? l0 : h0, l0, sel);
-                const uint32_t p1 = __builtin_amdgcn_perm(kb < 4 ? l1 : h1, l1, sel);
+                // v_perm bytes 0-3 are its second operand (l), 4-7 its first (h); 0x0c gives zero
+                const uint32_t sel = 0x0c000c00u | (uint32_t)c | ((uint32_t)kb << 16);
+                const uint32_t p0 = __builtin_amdgcn_perm(h0, l0, sel);
+                const uint32_t p1 = __builtin_amdgcn_perm(h1, l1, sel);
                 out[k * CN + c] = dot2(p0, wr0, dot2(p1, wr1, 1u << 9)) >> 10;
             }
             continue;
