@@ -24,8 +24,8 @@ namespace usv {
 namespace {
 
 constexpr int kHsvShift = 12;
-#ifndef USV_PREP_FAST
-#define USV_PREP_FAST 1  // equalize: wave-level LUT scan (2 barriers instead of 16), single-step hue wrap
+#ifndef USV_PREP_THREADS
+#define USV_PREP_THREADS 1024  // threads per block of the two frame-prep kernels
 #endif
 #ifndef USV_PREP_EXP
 #define USV_PREP_EXP 0  // timing experiments only (wrong results): 1 no global bin atomics, 2 no LDS atomics, 3 neither,
@@ -45,17 +45,33 @@ __device__ __forceinline__ void bgr2hsv_px(int b, int g, int r, const int* sdiv,
     h = min(max(h, 0), 255);
 }
 
-// RGB2HSV_b tables: cvRound((255 << 12) / i), cvRound((180 << 12) / (6 i)), entry 0 = 0.
+// RGB2HSV_b tables: cvRound((255 << 12) / i), cvRound((180 << 12) / (6 i)), entry 0 = 0.  Built at
+// compile time (IEEE double division as at run time; no quotient is an exact half, so rounding half
+// up equals cvRound's half-to-even here) and copied into LDS per block: the round-2 kernel computed
+// 512 f64 divisions per block.
+struct HsvTables {
+    int sdiv[256], hdiv[256];
+};
+constexpr HsvTables make_hsv_tables() {
+    HsvTables t{};
+    for (int i = 1; i < 256; ++i) {
+        t.sdiv[i] = (int)((255 << kHsvShift) / (1. * i) + 0.5);
+        t.hdiv[i] = (int)((180 << kHsvShift) / (6. * i) + 0.5);
+    }
+    return t;
+}
+__constant__ HsvTables c_hsv_tables = make_hsv_tables();
+static_assert(make_hsv_tables().sdiv[7] == 149211 && make_hsv_tables().hdiv[7] == 17554, "cvRound values");
+
 __device__ void hsv_tables(int* sdiv, int* hdiv) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        sdiv[i] = i ? __double2int_rn((255 << kHsvShift) / (1. * i)) : 0;
-        hdiv[i] = i ? __double2int_rn((180 << kHsvShift) / (6. * i)) : 0;
+        sdiv[i] = c_hsv_tables.sdiv[i];
+        hdiv[i] = c_hsv_tables.hdiv[i];
     }
 }
 
 __device__ __forceinline__ int round_u8(float f) { return min(max(__float2int_rn(f), 0), 255); }
 
-#if USV_PREP_FAST
 // Branchless HSV2BGR (the same float operations and the same selected taps as OpenCV's HSV2RGB_f, so
 // bit-identical): a wave holds all six sectors on real frames, and the switch / s == 0 branches ran as
 // divergent paths.  With s == 0 every tap equals v exactly (v * (1 - 0 * x) == v), so that branch
@@ -77,46 +93,6 @@ __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int&
     og = round_u8(g * 255.f);
     orr = round_u8(r * 255.f);
 }
-#else
-__device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int& og, int& orr) {
-    float h = (float)H8, s = S8 * (1.f / 255.f), v = V8 * (1.f / 255.f);
-    float b, g, r;
-    if (s == 0) {
-        b = g = r = v;
-    } else {
-        const float hscale = 6.f / 180;
-        h *= hscale;
-#if USV_PREP_FAST
-        // H8 is a byte: h in [0, 8.5], so OpenCV's wrap loops run at most one subtraction
-        if (h >= 6) h -= 6;
-#else
-        if (h < 0)
-            do h += 6; while (h < 0);
-        else if (h >= 6)
-            do h -= 6; while (h >= 6);
-#endif
-        int sector = (int)floorf(h);
-        h -= sector;
-        if ((unsigned)sector >= 6u) {
-            sector = 0;
-            h = 0.f;
-        }
-        const float t0 = v, t1 = v * (1.f - s), t2 = v * (1.f - s * h), t3 = v * (1.f - s * (1.f - h));
-        // sector_data {1,3,0} {1,0,2} {3,0,1} {0,2,1} {0,1,3} {2,1,0} -> (b, g, r) taps
-        switch (sector) {
-            case 0: b = t1; g = t3; r = t0; break;
-            case 1: b = t1; g = t0; r = t2; break;
-            case 2: b = t3; g = t0; r = t1; break;
-            case 3: b = t0; g = t2; r = t1; break;
-            case 4: b = t0; g = t1; r = t3; break;
-            default: b = t2; g = t1; r = t0; break;
-        }
-    }
-    ob = round_u8(b * 255.f);
-    og = round_u8(g * 255.f);
-    orr = round_u8(r * 255.f);
-}
-#endif
 
 // Work buffer (include/usv.h USV_FRAME_PREP_WORK_BYTES): per parity (the
 // caller alternates it between frames) kHistCopies 256-bin histograms; block
@@ -161,20 +137,22 @@ __device__ __forceinline__ void store_px4(uint8_t* p, const Px4& v, bool vec, in
 // row-by-row form with a fixed 256-block grid ran latency-bound.  When W % 4 == 0 and the rows are 4-byte aligned
 // every full sweep is straight-line vector code; the rest take a byte path.
 constexpr int kU = 2;
+constexpr int kPT = USV_PREP_THREADS;  // threads per block (frame prep)
+static_assert(kPT % 256 == 0 && kPT <= 1024, "whole 256-bin groups of threads");
 
 // for_each_quad(f): f(y, x, n, in) -> handles one quad; Load(y, x, n, vec) -> Px4.
 template <typename LoadF, typename BodyF>
 __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF load, BodyF body) {
     const int nq = (W + 3) >> 2;
     const int Q = nq * H;  // W * H <= 2^24
-    const int stride = gridDim.x * 256 * kU;
-    for (int base = blockIdx.x * 256 * kU + threadIdx.x; base < Q; base += stride) {
-        if (vec4 && base + (kU - 1) * 256 < Q) {
+    const int stride = gridDim.x * kPT * kU;
+    for (int base = blockIdx.x * kPT * kU + threadIdx.x; base < Q; base += stride) {
+        if (vec4 && base + (kU - 1) * kPT < Q) {
             int y[kU], x[kU];
             Px4 in[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const unsigned q = (unsigned)(base + u * 256);
+                const unsigned q = (unsigned)(base + u * kPT);
                 y[u] = (int)(q / (unsigned)nq);
                 x[u] = 4 * (int)(q - (unsigned)y[u] * (unsigned)nq);
                 in[u] = load(y[u], x[u], 4, true);
@@ -183,7 +161,7 @@ __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF loa
             for (int u = 0; u < kU; ++u) body(y[u], x[u], 4, true, in[u]);
         } else {
             for (int u = 0; u < kU; ++u) {
-                const int q = base + u * 256;
+                const int q = base + u * kPT;
                 if (q >= Q) break;
                 const int y = q / nq, x = 4 * (q - y * nq), n = min(4, W - x);
                 const bool v = vec4 && n == 4;
@@ -198,16 +176,16 @@ __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF loa
 // atomics); block 0 also clears histogram 1 - parity, which the previous
 // frame used and the next one will fill.  (A single "last block" ticket to
 // build the LUT here cost ~40 us: 512 returning atomics on one address.)
-__global__ __launch_bounds__(256) void hsv_hist_kernel(const uint8_t* __restrict__ bgr, int W, int H, int pitch,
+__global__ __launch_bounds__(kPT) void hsv_hist_kernel(const uint8_t* __restrict__ bgr, int W, int H, int pitch,
                                                        uint8_t* __restrict__ hsv, int hsv_pitch,
                                                        uint32_t* __restrict__ work, int parity, int vec) {
+    constexpr int NWV = kPT / 64;
     __shared__ int sdiv[256], hdiv[256];
-    __shared__ uint32_t lh[256];
-    const int t = threadIdx.x;
-    if (USV_PREP_EXP & 16) { sdiv[t] = 16 * t; hdiv[t] = 7 * t; }  // timing experiment: no per-block table build
-    else hsv_tables(sdiv, hdiv);
-    lh[t] = 0;
-    if (blockIdx.x == 0)
+    __shared__ uint32_t lh[NWV][256];  // one histogram per wave: its atomics never meet another wave's
+    const int t = threadIdx.x, wv = t >> 6;
+    hsv_tables(sdiv, hdiv);
+    for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
+    if (blockIdx.x == 0 && t < 256)
         for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
     __syncthreads();
     const bool vec4 = vec && (W & 3) == 0;
@@ -223,72 +201,70 @@ __global__ __launch_bounds__(256) void hsv_hist_kernel(const uint8_t* __restrict
                 out.c[3 * k] = h;
                 out.c[3 * k + 1] = sat;
                 out.c[3 * k + 2] = val;
-                if (!(USV_PREP_EXP & 2) && k < n) atomicAdd(&lh[val], 1u);
+                if (!(USV_PREP_EXP & 2) && k < n) atomicAdd(&lh[wv][val], 1u);
             }
             store_px4(hsv + (size_t)y * hsv_pitch + 3 * x, out, v, n);
         });
     __syncthreads();
-    if (!(USV_PREP_EXP & 1) && lh[t])
-        atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blockIdx.x % kHistCopies) + t], lh[t]);
+    if (t < 256) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) sum += lh[w][t];
+        if (!(USV_PREP_EXP & 1) && sum)
+            atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blockIdx.x % kHistCopies) + t], sum);
+    }
 }
 
 // V' = LUT[V] written back into hsv, HSV2BGR, BGR2GRAY; kU quads per thread.
-__global__ __launch_bounds__(256) void equalize_kernel(const uint32_t* __restrict__ work, int parity, int W, int H,
+__global__ __launch_bounds__(kPT) void equalize_kernel(const uint32_t* __restrict__ work, int parity, int W, int H,
                                                        uint8_t* __restrict__ hsv, int hsv_pitch,
                                                        uint8_t* __restrict__ bgr, int bgr_pitch,
                                                        uint8_t* __restrict__ gray, int gray_pitch, int vec) {
-    // equalizeHist's LUT from the complete histogram (every block builds it:
-    // an inclusive scan in LDS, then OpenCV's float scale and cvRound)
+    // equalizeHist's LUT from the complete histogram, built by the block's first 256 threads: an
+    // inclusive scan within each wave by shuffles plus the four wave totals, then OpenCV's float
+    // scale and cvRound
     __shared__ int scan[256];
     __shared__ int first;
     __shared__ uint8_t lut[256];
-    const int t = threadIdx.x;
-    int hv = 0;
-#pragma unroll
-    for (int c = 0; c < kHistCopies; ++c) hv += (int)work[kWHist + kParityWords * parity + 256 * c + t];
-#if USV_PREP_FAST
-    // inclusive scan of the 256 bins: within each wave by shuffles, then the waves' totals
     __shared__ int wsum[4], wfirst[4];
-    const int lane = t & 63, wv = t >> 6;
-    int x = hv;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int x = 0;
+    if (t < 256) {
+        int hv = 0;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    const unsigned long long nz = __ballot(hv != 0);
-    if (lane == 63) wsum[wv] = x;
-    if (lane == 0) wfirst[wv] = nz ? 64 * wv + __ffsll((long long)nz) - 1 : 256;
-    __syncthreads();
-    for (int k = 0; k < wv; ++k) x += wsum[k];
-    scan[t] = x;
-    if (t == 0) first = min(min(wfirst[0], wfirst[1]), min(wfirst[2], wfirst[3]));
-    __syncthreads();
-#else
-    if (t == 0) first = 256;
-    scan[t] = hv;
-    __syncthreads();
-    if (hv) atomicMin(&first, t);
-    for (int off = 1; off < 256; off <<= 1) {
-        const int add = t >= off ? scan[t - off] : 0;
-        __syncthreads();
-        scan[t] += add;
-        __syncthreads();
-    }
-#endif
-    const int total = W * H, i0 = first;
-    int lv = 0;
-    if (i0 < 256) {
-        const int h0 = scan[i0] - (i0 ? scan[i0 - 1] : 0);
-        if (h0 == total) {
-            lv = t == i0 ? i0 : 0;  // dst.setTo(i0)
-        } else if (t > i0) {
-            const float scale = (256 - 1.f) / (total - h0);
-            const int acc = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
-            lv = min(max(__float2int_rn(acc * scale), 0), 255);
+        for (int c = 0; c < kHistCopies; ++c) hv += (int)work[kWHist + kParityWords * parity + 256 * c + t];
+        x = hv;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
         }
+        const unsigned long long nz = __ballot(hv != 0);
+        if (lane == 63) wsum[wv] = x;
+        if (lane == 0) wfirst[wv] = nz ? 64 * wv + __ffsll((long long)nz) - 1 : 256;
     }
-    lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept, result unused)
+    __syncthreads();
+    if (t < 256) {
+        for (int k = 0; k < wv; ++k) x += wsum[k];
+        scan[t] = x;
+        if (t == 0) first = min(min(wfirst[0], wfirst[1]), min(wfirst[2], wfirst[3]));
+    }
+    __syncthreads();
+    if (t < 256) {
+        const int total = W * H, i0 = first;
+        int lv = 0;
+        if (i0 < 256) {
+            const int h0 = scan[i0] - (i0 ? scan[i0 - 1] : 0);
+            if (h0 == total) {
+                lv = t == i0 ? i0 : 0;  // dst.setTo(i0)
+            } else if (t > i0) {
+                const float scale = (256 - 1.f) / (total - h0);
+                const int acc = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
+                lv = min(max(__float2int_rn(acc * scale), 0), 255);
+            }
+        }
+        lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept, result unused)
+    }
     __syncthreads();
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
@@ -432,7 +408,7 @@ __global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
 
 // one sweep of kU quads per thread, at most 4096 blocks (larger frames loop)
 int prep_blocks(int W, int H) {
-    const long long q = (long long)((W + 3) / 4) * H, per = 256LL * kU;
+    const long long q = (long long)((W + 3) / 4) * H, per = (long long)kPT * kU;
     return (int)std::min<long long>(4096, std::max<long long>(1, (q + per - 1) / per));
 }
 
@@ -451,7 +427,7 @@ usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint
         (long long)W * H > (1LL << 24) || !al4(work) || (parity != 0 && parity != 1))
         return USV_ERR_INVALID_ARG;
     const int vec = al4(bgr) && al4(hsv) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(usv::prep_blocks(W, H)), dim3(256), 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(usv::prep_blocks(W, H)), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream),
                        bgr, W, H, pitch, hsv, hsv_pitch, static_cast<uint32_t*>(work), parity, vec);
     return usv::st(hipGetLastError());
 }
@@ -464,7 +440,7 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
         return USV_ERR_INVALID_ARG;
     const int vec = al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
                     gray_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(usv::prep_blocks(W, H)), dim3(256), 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(usv::equalize_kernel, dim3(usv::prep_blocks(W, H)), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream),
                        static_cast<const uint32_t*>(work), parity, W, H, hsv, hsv_pitch, bgr_out, bgr_pitch, gray,
                        gray_pitch, vec);
     return usv::st(hipGetLastError());
