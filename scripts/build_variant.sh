@@ -9,8 +9,9 @@ SRC=${VARIANT_SRC:-usv_sad_fast}   # which kernel file the defines apply to
 C=unsynchronized_stereo_vision_proj325_amd/csrc
 make -s -C $C
 mkdir -p build_variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -ffp-contract=off "$@" \
-    -c $C/$SRC.hip -o build_variants/$name.var.o
+# VARIANT_FILE: compile this file in place of $C/$SRC.hip (e.g. an older revision from git show)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -I$C -ffp-contract=off "$@" \
+    -c ${VARIANT_FILE:-$C/$SRC.hip} -o build_variants/$name.var.o
 objs=$(ls $C/build/*.o | grep -v "/$SRC.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.var.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f build_variants/$name.var.o
