@@ -13,6 +13,7 @@
 
 #include "usv.h"
 #include "usv_kernels.hpp"
+#include "usv_remap.hpp"
 
 namespace usv {
 namespace {
@@ -66,175 +67,37 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
     }
 }
 
-struct RemapJob {
-    const uint8_t* src;
-    int spitch;
-    const int16_t* map1;
-    const uint16_t* map2;
-    uint8_t* dst;
-    int dpitch;
-};
-
-// QPT quads (4 output pixels each) per thread over a flat range of quads per camera.  Per thread
-// every load is issued before any arithmetic: the maps of all its quads (one 16-B and one 8-B load
-// per quad when the rows are 4-pixel aligned), then, for every pixel, the two aligned source reads
-// (2 dwords for gray, 3 for BGR per row) at an address clamped into the image, so the reads are
-// unconditional straight-line code; a pixel whose taps are not all inside the image (or whose
-// aligned read was clamped) is redone afterwards on a per-tap path that reads 0 outside.  The
-// result leaves as one 4-B (gray) or one 12-B (BGR) store per quad.
-//   * Blocks are numbered XCD-contiguously (block b runs on XCD b % 8, and XCD k takes the k-th
-//     contiguous run of quads), so the source rows one output band reads are fetched into one L2.
-//   * Fixed point: every weight of OpenCV's bilinear table is a multiple of 32 and the four sum to
-//     32768, so (S00 w0 + S01 w1 + S10 w2 + S11 w3 + 2^14) >> 15 = (S00 a0 + ... + 2^9) >> 10 with
-//     a = w / 32 <= 1024: products < 2^18, sums < 2^24 and never above 255 after the shift.  The
-//     two taps of a row are one u16 pair and their weights another, so each channel is two
-//     v_dot2_u32_u16.
-//   * Source offsets are 32-bit (sy * pitch + byte, a 24-bit multiply) from the job's base pointer.
-typedef unsigned short usv_us2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t dot2(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_udot2(__builtin_bit_cast(usv_us2, a), __builtin_bit_cast(usv_us2, b), c, false);
-}
-
-#ifndef USV_REMAP_QPT
-#define USV_REMAP_QPT 1  // quads per thread (2: 18.1 us, 4: 24.6 us vs 15.1 us at 1, 1080p BGR pair, one box)
-#endif
-constexpr int kRemapQPT = USV_REMAP_QPT;
-
+// One quad (4 output pixels) per thread over a flat, XCD-contiguous range of quads per camera;
+// remap_quad (usv_remap.hpp) computes it, the result leaves as one 4-B (gray) or one 12-B (BGR)
+// store.  (Two or four quads per thread with every load issued first ran slower: 18.1 / 24.6 us
+// vs 15.1 us for the 1080p BGR pair on one box.)
 template <int CN>
 __global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
                                                     unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
-    constexpr int QPT = kRemapQPT, NWD = CN == 1 ? 2 : 3;
-    const unsigned total = gridDim.x, lin = blockIdx.x;
-    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-    const unsigned lb = xcd * base + min(xcd, rem) + (lin >> 3);
+    const unsigned lb = xcd_block(blockIdx.x, gridDim.x);
     const unsigned job = lb >= blocks_per_job ? 1u : 0u;
     const RemapJob& j = job ? j1 : j0;
-    const unsigned nq = (unsigned)(W + 3) >> 2, nqt = nq * (unsigned)H;
-    const unsigned qb = (lb - job * blocks_per_job) * (256u * QPT) + threadIdx.x;
-    int yq[QPT], xq[QPT], nn[QPT];
-    int mx[QPT][4], my[QPT][4], mf[QPT][4];
-#pragma unroll
-    for (int u = 0; u < QPT; ++u) {
-        const unsigned q = qb + 256u * u;
-        const bool ok = q < nqt;
-        const int y = ok ? (int)(q / nq) : 0;
-        const int x0 = ok ? 4 * (int)(q - (unsigned)y * nq) : 0;
-        yq[u] = y;
-        xq[u] = x0;
-        nn[u] = ok ? min(4, W - x0) : 0;
-        const size_t mrow = (size_t)y * W + x0;
-        if (vec_map && nn[u] == 4) {
-            const int4 a = *reinterpret_cast<const int4*>(j.map1 + 2 * mrow);
-            const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
-            const int w4[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                mx[u][k] = (int)(int16_t)(w4[k] & 0xFFFF);
-                my[u][k] = (int)(int16_t)((unsigned)w4[k] >> 16);
-            }
-            mf[u][0] = f.x & 0xFFFF;
-            mf[u][1] = f.x >> 16;
-            mf[u][2] = f.y & 0xFFFF;
-            mf[u][3] = f.y >> 16;
+    const unsigned nq = (unsigned)(W + 3) >> 2;
+    const unsigned q = (lb - job * blocks_per_job) * 256u + threadIdx.x;
+    if (q >= nq * (unsigned)H) return;
+    const int y = (int)(q / nq);
+    const int x0 = 4 * (int)(q - (unsigned)y * nq);
+    const int n = min(4, W - x0);
+    uint32_t out[4 * CN];
+    remap_quad<CN>(j, sW, sH, W, y, x0, n, vec_map, vec_src, out);
+    uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
+    if (vec_dst && n == 4) {
+        if constexpr (CN == 3) {
+            uint3 w;
+            w.x = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+            w.y = out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24);
+            w.z = out[8] | (out[9] << 8) | (out[10] << 16) | (out[11] << 24);
+            *reinterpret_cast<uint3*>(d) = w;
         } else {
-            for (int k = 0; k < 4; ++k) {
-                const int kk = k < nn[u] ? k : 0;
-                mx[u][k] = nn[u] ? j.map1[2 * (mrow + kk)] : -2;  // an idle slot: outside, nothing stored
-                my[u][k] = nn[u] ? j.map1[2 * (mrow + kk) + 1] : -2;
-                mf[u][k] = nn[u] ? j.map2[mrow + kk] : 0;
-            }
+            *reinterpret_cast<uint32_t*>(d) = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
         }
-    }
-    // unconditional aligned reads at clamped addresses (rows sy, sy + 1 and bytes a .. a + 4 NWD - 1
-    // always inside the source)
-    const int amax = (j.spitch - 4 * NWD) & ~3;
-    uint32_t u0[QPT][4][NWD], u1[QPT][4][NWD];
-    uint32_t good = 0;  // bit (4u + k): the clamped read is the exact one and every tap is inside
-#pragma unroll
-    for (int u = 0; u < QPT; ++u) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!vec_src) {  // (uniform) unaligned source: every pixel takes the per-tap path
-#pragma unroll
-                for (int i = 0; i < NWD; ++i) u0[u][k][i] = u1[u][k][i] = 0;
-                continue;
-            }
-            const int sx = mx[u][k], sy = my[u][k];
-            const int a = (sx * CN) & ~3;
-            const int ac = min(max(a, 0), amax), yc = min(max(sy, 0), sH - 2 > 0 ? sH - 2 : 0);
-            const bool in = sx >= 0 && sx + 1 < sW && sy >= 0 && sy + 1 < sH && a == ac;
-            good |= in ? 1u << (4 * u + k) : 0u;
-            const uint32_t r0 = __umul24((uint32_t)yc, (uint32_t)j.spitch) + (uint32_t)ac;  // both < 2^24 (launch)
-            const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
-            const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r0 + (uint32_t)(sH > 1 ? j.spitch : 0));
-#pragma unroll
-            for (int i = 0; i < NWD; ++i) {
-                u0[u][k][i] = q0[i];
-                u1[u][k][i] = q1[i];
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < QPT; ++u) {
-        uint32_t out[4 * CN];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t ty = (uint32_t)mf[u][k] >> 5, tx = (uint32_t)mf[u][k] & 31u;
-            // row weights as u16 pairs: (32 - tx, tx) scaled by (32 - ty) for row 0, by ty for row 1
-            const uint32_t wx = (32u - tx) | (tx << 16);
-            const uint32_t wr0 = wx * (32u - ty), wr1 = wx * ty;  // both halves <= 1024: no carry
-            const int o = (mx[u][k] * CN) & 3;
-            const uint32_t l0 = __builtin_amdgcn_alignbyte(u0[u][k][1], u0[u][k][0], o);  // tap bytes 0..3
-            const uint32_t l1 = __builtin_amdgcn_alignbyte(u1[u][k][1], u1[u][k][0], o);
-            uint32_t h0 = 0, h1 = 0;
-            if constexpr (CN == 3) {
-                h0 = __builtin_amdgcn_alignbyte(u0[u][k][2], u0[u][k][1], o);  // tap bytes 4..7
-                h1 = __builtin_amdgcn_alignbyte(u1[u][k][2], u1[u][k][1], o);
-            }
-#pragma unroll
-            for (int c = 0; c < CN; ++c) {
-                // (left tap | right tap << 16) of each row: byte c and byte CN + c of (h:l); v_perm bytes
-                // 0-3 are its second operand, 4-7 its first, 0x0c gives zero
-                const uint32_t sel = 0x0c000c00u | (uint32_t)c | ((uint32_t)(CN + c) << 16);
-                const uint32_t p0 = __builtin_amdgcn_perm(h0, l0, sel);
-                const uint32_t p1 = __builtin_amdgcn_perm(h1, l1, sel);
-                out[k * CN + c] = dot2(p0, wr0, dot2(p1, wr1, 1u << 9)) >> 10;
-            }
-            if (!(good >> (4 * u + k) & 1u)) {
-                // border / clamped read: per-tap reads, 0 outside (BORDER_CONSTANT), all four outside -> 0
-                const int sx = mx[u][k], sy = my[u][k];
-                const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
-                const bool any = sx < sW && sx + 1 >= 0 && sy < sH && sy + 1 >= 0;
-                const uint8_t* rp0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
-                const uint8_t* rp1 = rp0 + j.spitch;
-                const uint32_t w0 = wr0 & 0xFFFFu, w1 = wr0 >> 16, w2 = wr1 & 0xFFFFu, w3 = wr1 >> 16;
-#pragma unroll
-                for (int c = 0; c < CN; ++c) {
-                    const uint32_t v0 = (any && x0ok && y0ok) ? rp0[c] : 0;
-                    const uint32_t v1 = (any && x1ok && y0ok) ? rp0[CN + c] : 0;
-                    const uint32_t v2 = (any && x0ok && y1ok) ? rp1[c] : 0;
-                    const uint32_t v3 = (any && x1ok && y1ok) ? rp1[CN + c] : 0;
-                    out[k * CN + c] =
-                        (__umul24(v0, w0) + __umul24(v1, w1) + __umul24(v2, w2) + __umul24(v3, w3) + (1u << 9)) >> 10;
-                }
-            }
-        }
-        const int n = nn[u];
-        if (n == 0) continue;
-        uint8_t* d = j.dst + (size_t)yq[u] * j.dpitch + (size_t)xq[u] * CN;
-        if (vec_dst && n == 4) {
-            if constexpr (CN == 3) {
-                uint3 w;
-                w.x = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
-                w.y = out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24);
-                w.z = out[8] | (out[9] << 8) | (out[10] << 16) | (out[11] << 24);
-                *reinterpret_cast<uint3*>(d) = w;
-            } else {
-                *reinterpret_cast<uint32_t*>(d) = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
-            }
-        } else {
-            for (int b = 0; b < n * CN; ++b) d[b] = (uint8_t)out[b];
-        }
+    } else {
+        for (int b = 0; b < n * CN; ++b) d[b] = (uint8_t)out[b];
     }
 }
 
@@ -254,7 +117,7 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
         a.spitch >= (1 << 24) || b.spitch >= (1 << 24))
         return USV_ERR_UNSUPPORTED;
     const long long quads = (long long)((W + 3) / 4) * H;
-    const long long per_job = (quads + 256 * kRemapQPT - 1) / (256 * kRemapQPT);
+    const long long per_job = (quads + 255) / 256;
     if (a.spitch < 4 * (cn == 1 ? 2 : 3) || b.spitch < 4 * (cn == 1 ? 2 : 3)) vec_src = false;  // rows too short for the aligned reads
     if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
     dim3 grid((unsigned)(per_job * n_jobs)), block(256);
