@@ -192,7 +192,7 @@ def time_launches(fn, steps: int, stream) -> float:
 def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
     """The per-frame stages around the block matcher, config C geometry,
     synthetic BGR frames and calibration; each leg's roofline is HBM (algorithmic bytes / avg launch)."""
-    from unsynchronized_stereo_vision_proj325_amd.preproc import ABSDiffSearch, FramePrep
+    from unsynchronized_stereo_vision_proj325_amd.preproc import ABSDiffSearch, FramePrep, FramePrepPair
     from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
 
     rng = np.random.default_rng(7)
@@ -216,6 +216,14 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
         # absdiff + threshold + erode + dilate: gray + prev in, mask out
         "motion_mask": (lambda: ABSDiffSearch(gray, prev, out=mask), px * 3),
     }
+    pair = FramePrepPair(dev)
+    pouts = [torch.empty_like(src_l) for _ in range(4)] + [torch.empty((H, W), dtype=torch.uint8, device=dev)
+                                                          for _ in range(2)]
+    # both cameras' frame prep in two launches (usv_frame_prep_pair_u8)
+    legs["frame_prep_pair"] = (lambda: pair(out_l, out_r, outs=pouts), 2 * px * (3 + 3 + 3 + 7))
+    # the whole per-frame stage of the pair in two launches (usv_rectify_prep_pair_u8): rectify + HSV +
+    # histogram (6 map + 3 src + 3 hsv), then equalize / HSV2BGR / gray (3 + 3 + 3 + 1), per camera
+    legs["rectify_prep_pair"] = (lambda: pair.rectify_prep(rl, rr, src_l, src_r, outs=pouts), 2 * px * (12 + 10))
     res = {}
     for name, (fn, nbytes) in legs.items():
         us = time_launches(fn, steps, s)
@@ -381,6 +389,43 @@ def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
     return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
             "stages": "rectify pair (BGR) -> frame prep x2 -> SAD w=%d D=%d -> distance map" % (w, D),
             "launches_per_frame": 1 + 2 * 2 + 1}
+
+
+def frame_chain_fused_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
+    """The per-frame chain with the fused stage: usv_rectify_prep_pair_u8 (rectify + HSV + histogram of
+    both cameras, then equalize / HSV2BGR / gray of both) -> SAD block match -> distance map: three
+    launches per frame instead of six.  Checked against the six-launch chain on the same input."""
+    from unsynchronized_stereo_vision_proj325_amd.preproc import FramePrep, FramePrepPair
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
+
+    rng = np.random.default_rng(11)
+    cl, cr = synthetic_calibration(W, H, seed=2)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
+    pair = FramePrepPair(dev)
+    outs = [torch.empty_like(src_l) for _ in range(4)] + [torch.empty((H, W), dtype=torch.uint8, device=dev)
+                                                         for _ in range(2)]
+    disp = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    dist = torch.empty((H, W), dtype=torch.float64, device=dev)
+    matcher = StereoBlockMatcher(D, w)
+
+    def frame():
+        pair.rectify_prep(rl, rr, src_l, src_r, outs=outs)
+        matcher.compute(outs[4], outs[5], with_distance=True, out_disp=disp, out_dist=dist)
+
+    frame()
+    torch.cuda.synchronize()
+    got = disp.clone()
+    rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)
+    rectify_pair(rl, rr, src_l, src_r, rect_l, rect_r)
+    gl = FramePrep(dev)(rect_l)[2]
+    gr = FramePrep(dev)(rect_r)[2]
+    same = bool(torch.equal(got, matcher.compute(gl, gr)))
+    us = time_launches(frame, steps, torch.cuda.current_stream())
+    return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
+            "stages": "rectify + HSV + hist (pair) -> equalize/HSV2BGR/gray (pair) -> SAD w=%d D=%d -> distance "
+                      "map" % (w, D), "launches_per_frame": 3, "matches_six_launch_chain": same}
 
 
 def frame_chain_graph_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
@@ -766,6 +811,7 @@ def main():
         rec["e2e"] = e2e_leg(dev, L, R, D, w, a.extra_steps)
         rec["frame_chain"] = frame_chain_leg(dev, W, H, D, w, a.extra_steps)
         rec["frame_chain_graph"] = frame_chain_graph_leg(dev, W, H, D, w, a.extra_steps)
+        rec["frame_chain_fused"] = frame_chain_fused_leg(dev, W, H, D, w, a.extra_steps)
         rec["fallbacks"] = fallback_legs(dev, L, R, D, w, max(2, a.extra_steps // 4))
         rec["matcher"] = matcher_leg(dev)
     if world == 1 and rank == 0 and not a.no_cpu_baseline:

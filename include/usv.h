@@ -389,6 +389,23 @@ usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_
                              int hsv_pitch, uint8_t* bgr_out, int bgr_pitch, uint8_t* gray,
                              int gray_pitch, void* work, int parity, void* stream);
 
+/* Both cameras of a pair in two launches (the two calls above, each camera with its own half of
+ * `work`, which holds 2 * USV_FRAME_PREP_WORK_BYTES bytes). */
+usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int W, int H, int pitch, uint8_t* hsvL,
+                                  uint8_t* hsvR, int hsv_pitch, uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch,
+                                  uint8_t* grayL, uint8_t* grayR, int gray_pitch, void* work, int parity,
+                                  void* stream);
+/* The whole per-frame stage of a pair in two launches (P/Main.cpp:913-921): rectification (BGR,
+ * remap INTER_LINEAR of src with each camera's CV_16SC2 map) fused with BGR2HSV and the histogram,
+ * then equalize + HSV2BGR + BGR2GRAY.  Bit-identical to usv_rectify_pair_u8 (cn = 3) followed by
+ * usv_frame_prep_pair_u8, without the rectified-BGR intermediate (the reference overwrites it,
+ * P/Main.cpp:370).  work: 2 * USV_FRAME_PREP_WORK_BYTES bytes (camera L, then R). */
+usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                    const int16_t* map1L, const uint16_t* map2L, const int16_t* map1R,
+                                    const uint16_t* map2R, int W, int H, uint8_t* hsvL, uint8_t* hsvR, int hsv_pitch,
+                                    uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch, uint8_t* grayL,
+                                    uint8_t* grayR, int gray_pitch, void* work, int parity, void* stream);
+
 /* |gray - prev| > thresh -> 255, then erode + dilate with the 5x5 ellipse
  * (gray and prev share pitch). */
 usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch,

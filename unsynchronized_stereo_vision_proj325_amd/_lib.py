@@ -124,6 +124,12 @@ SIGNATURES = {
                                              c_void_p, c_int, c_void_p]),
     "usv_frame_prep_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                   c_int, c_void_p, c_int, c_void_p]),
+    "usv_frame_prep_pair_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                       c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                       c_void_p]),
+    "usv_rectify_prep_pair_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                         c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "usv_motion_mask_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "usv_load_calibration": (c_int, [c_char_p, POINTER(usv_calibration)]),
     "usv_calibration_rectify_params": (c_int, [POINTER(usv_calibration), c_int, c_void_p]),

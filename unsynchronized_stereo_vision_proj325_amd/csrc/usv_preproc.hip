@@ -26,7 +26,7 @@ namespace usv {
 namespace {
 
 #ifndef USV_PREP_THREADS
-#define USV_PREP_THREADS 1024  // threads per block of the two frame-prep kernels
+#define USV_PREP_THREADS 256  // threads per block of the two frame-prep kernels (512 / 1024 ran slower)
 #endif
 #ifndef USV_PREP_EXP
 #define USV_PREP_EXP 0  // timing experiments only (wrong results): 1 no global bin atomics, 2 no LDS atomics, 3 neither,
@@ -80,32 +80,43 @@ constexpr int kU = 2;
 constexpr int kPT = USV_PREP_THREADS;  // threads per block (frame prep)
 static_assert(kPT % 256 == 0 && kPT <= 1024, "whole 256-bin groups of threads");
 
-// for_each_quad(f): f(y, x, n, in) -> handles one quad; Load(y, x, n, vec) -> Px4.
-template <typename LoadF, typename BodyF>
-__device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF load, BodyF body) {
+// for_each_quad: body(y, x, n, vec, in) handles one quad, load(y, x, n, vec) -> Px4 reads it.  Block
+// blk of nblk (a job's share of the grid) sweeps quads blk * kPT * kU + threadIdx.x + u * kPT; the
+// first sweep's loads are issued BEFORE prologue() (the block's table / LUT set-up, which ends in a
+// barrier every thread reaches), so the two latencies overlap instead of adding.
+template <typename LoadF, typename PrologueF, typename BodyF>
+__device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, int blk, int nblk, LoadF load,
+                                              PrologueF prologue, BodyF body) {
     const int nq = (W + 3) >> 2;
     const int Q = nq * H;  // W * H <= 2^24
-    const int stride = gridDim.x * kPT * kU;
-    for (int base = blockIdx.x * kPT * kU + threadIdx.x; base < Q; base += stride) {
-        if (vec4 && base + (kU - 1) * kPT < Q) {
-            int y[kU], x[kU];
-            Px4 in[kU];
+    const int stride = nblk * kPT * kU;
+    int base = blk * kPT * kU + threadIdx.x;
+    int y[kU], x[kU];
+    Px4 in[kU];
+    auto full = [&](int b) { return vec4 && b + (kU - 1) * kPT < Q; };
+    auto issue = [&](int b) {
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const unsigned q = (unsigned)(base + u * kPT);
-                y[u] = (int)(q / (unsigned)nq);
-                x[u] = 4 * (int)(q - (unsigned)y[u] * (unsigned)nq);
-                in[u] = load(y[u], x[u], 4, true);
-            }
+        for (int u = 0; u < kU; ++u) {
+            const unsigned q = (unsigned)(b + u * kPT);
+            y[u] = (int)(q / (unsigned)nq);
+            x[u] = 4 * (int)(q - (unsigned)y[u] * (unsigned)nq);
+            in[u] = load(y[u], x[u], 4, true);
+        }
+    };
+    if (full(base)) issue(base);
+    prologue();
+    for (bool first = true; base < Q; base += stride, first = false) {
+        if (full(base)) {
+            if (!first) issue(base);
 #pragma unroll
             for (int u = 0; u < kU; ++u) body(y[u], x[u], 4, true, in[u]);
         } else {
             for (int u = 0; u < kU; ++u) {
                 const int q = base + u * kPT;
                 if (q >= Q) break;
-                const int y = q / nq, x = 4 * (q - y * nq), n = min(4, W - x);
+                const int yy = q / nq, xx = 4 * (q - yy * nq), n = min(4, W - xx);
                 const bool v = vec4 && n == 4;
-                body(y, x, n, v, load(y, x, n, v));
+                body(yy, xx, n, v, load(yy, xx, n, v));
             }
         }
     }
@@ -116,22 +127,37 @@ __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, LoadF loa
 // atomics); block 0 also clears histogram 1 - parity, which the previous
 // frame used and the next one will fill.  (A single "last block" ticket to
 // build the LUT here cost ~40 us: 512 returning atomics on one address.)
-__global__ __launch_bounds__(kPT) void hsv_hist_kernel(const uint8_t* __restrict__ bgr, int W, int H, int pitch,
-                                                       uint8_t* __restrict__ hsv, int hsv_pitch,
-                                                       uint32_t* __restrict__ work, int parity, int vec) {
+struct HistJob {
+    const uint8_t* bgr;
+    int pitch;
+    uint8_t* hsv;
+    int hsv_pitch;
+    uint32_t* work;
+};
+__global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, int W, int H, int parity,
+                                                       int blocks_per_job, int vec) {
     constexpr int NWV = kPT / 64;
+    const int job = (int)blockIdx.x >= blocks_per_job ? 1 : 0;
+    const int blk = (int)blockIdx.x - job * blocks_per_job;
+    const HistJob& j = job ? j1 : j0;
+    const uint8_t* __restrict__ bgr = j.bgr;
+    const int pitch = j.pitch, hsv_pitch = j.hsv_pitch;
+    uint8_t* __restrict__ hsv = j.hsv;
+    uint32_t* __restrict__ work = j.work;
     __shared__ int sdiv[256], hdiv[256];
     __shared__ uint32_t lh[NWV][256];  // one histogram per wave: its atomics never meet another wave's
     const int t = threadIdx.x, wv = t >> 6;
-    hsv_tables(sdiv, hdiv);
-    for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
-    if (blockIdx.x == 0 && t < 256)
-        for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
-    __syncthreads();
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
-        W, H, vec4,
+        W, H, vec4, blk, blocks_per_job,
         [&](int y, int x, int n, bool v) { return load_px4(bgr + (size_t)y * pitch + 3 * x, v, n); },
+        [&] {
+            hsv_tables(sdiv, hdiv);
+            for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
+            if (blk == 0 && t < 256)
+                for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
+            __syncthreads();
+        },
         [&](int y, int x, int n, bool v, const Px4& in) {
             Px4 out;
 #pragma unroll
@@ -151,65 +177,80 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(const uint8_t* __restrict
 #pragma unroll
         for (int w = 0; w < NWV; ++w) sum += lh[w][t];
         if (!(USV_PREP_EXP & 1) && sum)
-            atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blockIdx.x % kHistCopies) + t], sum);
+            atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blk % kHistCopies) + t], sum);
     }
 }
 
-// V' = LUT[V] written back into hsv, HSV2BGR, BGR2GRAY; kU quads per thread.
-__global__ __launch_bounds__(kPT) void equalize_kernel(const uint32_t* __restrict__ work, int parity, int W, int H,
-                                                       uint8_t* __restrict__ hsv, int hsv_pitch,
-                                                       uint8_t* __restrict__ bgr, int bgr_pitch,
-                                                       uint8_t* __restrict__ gray, int gray_pitch, int vec) {
-    // equalizeHist's LUT from the complete histogram, built by the block's first 256 threads: an
-    // inclusive scan within each wave by shuffles plus the four wave totals, then OpenCV's float
-    // scale and cvRound
+// One camera's equalize pass: the histogram it reads and the images it rewrites.
+struct EqJob {
+    const uint32_t* work;
+    uint8_t* hsv;
+    int hsv_pitch;
+    uint8_t* bgr;
+    int bgr_pitch;
+    uint8_t* gray;
+    int gray_pitch;
+};
+
+// V' = LUT[V] written back into hsv, HSV2BGR, BGR2GRAY; kU quads per thread.  Blocks
+// [0, blocks_per_job) take job j0, the rest j1 (both cameras of a pair in one launch).  The
+// equalizeHist LUT comes from the job's complete histogram, built by the block's first 256 threads
+// while the first sweep's pixel loads are in flight: an inclusive scan within each wave by shuffles
+// plus the four wave totals, then OpenCV's float scale and cvRound.
+__global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int parity, int W, int H,
+                                                       int blocks_per_job, int vec) {
     __shared__ int scan[256];
     __shared__ int first;
     __shared__ uint8_t lut[256];
     __shared__ int wsum[4], wfirst[4];
+    const int job = (int)blockIdx.x >= blocks_per_job ? 1 : 0;
+    const EqJob& j = job ? j1 : j0;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    int x = 0;
-    if (t < 256) {
-        int hv = 0;
+    auto build_lut = [&] {
+        int x = 0;
+        if (t < 256) {
+            int hv = 0;
 #pragma unroll
-        for (int c = 0; c < kHistCopies; ++c) hv += (int)work[kWHist + kParityWords * parity + 256 * c + t];
-        x = hv;
+            for (int c = 0; c < kHistCopies; ++c) hv += (int)j.work[kWHist + kParityWords * parity + 256 * c + t];
+            x = hv;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-        }
-        const unsigned long long nz = __ballot(hv != 0);
-        if (lane == 63) wsum[wv] = x;
-        if (lane == 0) wfirst[wv] = nz ? 64 * wv + __ffsll((long long)nz) - 1 : 256;
-    }
-    __syncthreads();
-    if (t < 256) {
-        for (int k = 0; k < wv; ++k) x += wsum[k];
-        scan[t] = x;
-        if (t == 0) first = min(min(wfirst[0], wfirst[1]), min(wfirst[2], wfirst[3]));
-    }
-    __syncthreads();
-    if (t < 256) {
-        const int total = W * H, i0 = first;
-        int lv = 0;
-        if (i0 < 256) {
-            const int h0 = scan[i0] - (i0 ? scan[i0 - 1] : 0);
-            if (h0 == total) {
-                lv = t == i0 ? i0 : 0;  // dst.setTo(i0)
-            } else if (t > i0) {
-                const float scale = (256 - 1.f) / (total - h0);
-                const int acc = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
-                lv = min(max(__float2int_rn(acc * scale), 0), 255);
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
             }
+            const unsigned long long nz = __ballot(hv != 0);
+            if (lane == 63) wsum[wv] = x;
+            if (lane == 0) wfirst[wv] = nz ? 64 * wv + __ffsll((long long)nz) - 1 : 256;
         }
-        lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept, result unused)
-    }
-    __syncthreads();
+        __syncthreads();
+        if (t < 256) {
+            for (int k = 0; k < wv; ++k) x += wsum[k];
+            scan[t] = x;
+            if (t == 0) first = min(min(wfirst[0], wfirst[1]), min(wfirst[2], wfirst[3]));
+        }
+        __syncthreads();
+        if (t < 256) {
+            const int total = W * H, i0 = first;
+            int lv = 0;
+            if (i0 < 256) {
+                const int h0 = scan[i0] - (i0 ? scan[i0 - 1] : 0);
+                if (h0 == total) {
+                    lv = t == i0 ? i0 : 0;  // dst.setTo(i0)
+                } else if (t > i0) {
+                    const float scale = (256 - 1.f) / (total - h0);
+                    const int acc = scan[t] - scan[i0];  // hist[i0 + 1 .. t]
+                    lv = min(max(__float2int_rn(acc * scale), 0), 255);
+                }
+            }
+            lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept)
+        }
+        __syncthreads();
+    };
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
-        W, H, vec4,
-        [&](int y, int x, int n, bool v) { return load_px4(hsv + (size_t)y * hsv_pitch + 3 * x, v, n); },
+        W, H, vec4, (int)blockIdx.x - job * blocks_per_job, blocks_per_job,
+        [&](int y, int x, int n, bool v) { return load_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, v, n); },
+        build_lut,
         [&](int y, int x, int n, bool v, Px4 in) {
             Px4 o;
             uint32_t g4 = 0;
@@ -224,12 +265,59 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(const uint32_t* __restric
                 o.c[3 * k + 2] = r;
                 g4 |= (uint32_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14) << (8 * k);
             }
-            store_px4(hsv + (size_t)y * hsv_pitch + 3 * x, in, v, n);
-            store_px4(bgr + (size_t)y * bgr_pitch + 3 * x, o, v, n);
-            uint8_t* go = gray + (size_t)y * gray_pitch + x;
+            store_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, in, v, n);
+            store_px4(j.bgr + (size_t)y * j.bgr_pitch + 3 * x, o, v, n);
+            uint8_t* go = j.gray + (size_t)y * j.gray_pitch + x;
             if (v) *reinterpret_cast<uint32_t*>(go) = g4;
             else for (int k = 0; k < n; ++k) go[k] = (uint8_t)(g4 >> (8 * k));
         });
+}
+
+// Fused first half of the per-frame chain for BOTH cameras (P/Main.cpp:913-919): rectify
+// (remap_quad: initUndistortRectifyMap map + remap INTER_LINEAR, P/Main.cpp:351-359), BGR2HSV and
+// the histogram of V, without writing the rectified BGR image the reference overwrites anyway
+// (LightingCorrection writes its HSV2BGR result back into CalibratedImg, P/Main.cpp:370).  One quad
+// per thread per iteration over the job's quads; per-wave LDS histograms, one global add per bin
+// and block into copy blockIdx % kHistCopies of the job's workspace (as hsv_hist_kernel).
+struct RectPrepJob {
+    RemapJob r;  // r.dst / r.dpitch: the HSV image
+    uint32_t* work;
+};
+__global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, RectPrepJob j1, int sW, int sH, int W,
+                                                               int H, int blocks_per_job, int vec_map, int vec_src,
+                                                               int vec_dst, int parity) {
+    __shared__ int sdiv[256], hdiv[256];
+    __shared__ uint32_t lh[4][256];
+    const unsigned lb = xcd_block(blockIdx.x, gridDim.x);
+    const int job = (int)lb >= blocks_per_job ? 1 : 0;
+    const RectPrepJob& j = job ? j1 : j0;
+    const int blk = (int)lb - job * blocks_per_job;
+    const int t = threadIdx.x, wv = t >> 6;
+    const int nq = (W + 3) >> 2, Q = nq * H;
+    hsv_tables(sdiv, hdiv);
+    for (int i = t; i < 4 * 256; i += 256) (&lh[0][0])[i] = 0;
+    if (blk == 0)
+        for (int c = 0; c < kHistCopies; ++c) j.work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
+    __syncthreads();
+    for (int q = blk * 256 + t; q < Q; q += blocks_per_job * 256) {
+        const int y = q / nq, x0 = 4 * (q - y * nq), n = min(4, W - x0);
+        uint32_t px[12];
+        remap_quad<3>(j.r, sW, sH, W, y, x0, n, vec_map, vec_src, px);
+        Px4 out;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int h, sat, val;
+            bgr2hsv_px((int)px[3 * k], (int)px[3 * k + 1], (int)px[3 * k + 2], sdiv, hdiv, h, sat, val);
+            out.c[3 * k] = h;
+            out.c[3 * k + 1] = sat;
+            out.c[3 * k + 2] = val;
+            if (k < n) atomicAdd(&lh[wv][val], 1u);
+        }
+        store_px4(j.r.dst + (size_t)y * j.r.dpitch + 3 * x0, out, vec_dst && n == 4, n);
+    }
+    __syncthreads();
+    const uint32_t sum = lh[0][t] + lh[1][t] + lh[2][t] + lh[3][t];
+    if (sum) atomicAdd(&j.work[kWHist + kParityWords * parity + 256 * (blockIdx.x % kHistCopies) + t], sum);
 }
 
 // ---- masks: threshold / inRange, then erode + dilate (5x5 ellipse) in one tile ----
@@ -367,8 +455,10 @@ usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint
         (long long)W * H > (1LL << 24) || !al4(work) || (parity != 0 && parity != 1))
         return USV_ERR_INVALID_ARG;
     const int vec = al4(bgr) && al4(hsv) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(usv::prep_blocks(W, H)), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream),
-                       bgr, W, H, pitch, hsv, hsv_pitch, static_cast<uint32_t*>(work), parity, vec);
+    const usv::HistJob j{bgr, pitch, hsv, hsv_pitch, static_cast<uint32_t*>(work)};
+    const int nb = usv::prep_blocks(W, H);
+    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j, W, H,
+                       parity, nb, vec);
     return usv::st(hipGetLastError());
 }
 
@@ -380,9 +470,10 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
         return USV_ERR_INVALID_ARG;
     const int vec = al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
                     gray_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(usv::prep_blocks(W, H)), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream),
-                       static_cast<const uint32_t*>(work), parity, W, H, hsv, hsv_pitch, bgr_out, bgr_pitch, gray,
-                       gray_pitch, vec);
+    const usv::EqJob j{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch};
+    const int nb = usv::prep_blocks(W, H);
+    hipLaunchKernelGGL(usv::equalize_kernel, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j,
+                       parity, W, H, nb, vec);
     return usv::st(hipGetLastError());
 }
 
@@ -393,6 +484,65 @@ usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_
     if (r != USV_OK) return r;
     return usv_equalize_hsv_bgr_gray_u8(work, parity, hsv, W, H, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
                                         stream);
+}
+
+usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int W, int H, int pitch, uint8_t* hsvL,
+                                  uint8_t* hsvR, int hsv_pitch, uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch,
+                                  uint8_t* grayL, uint8_t* grayR, int gray_pitch, void* work, int parity,
+                                  void* stream) {
+    if (!bgrL || !bgrR || !hsvL || !hsvR || !bgr_outL || !bgr_outR || !grayL || !grayR || !work || W <= 0 ||
+        H <= 0 || pitch < 3 * W || hsv_pitch < 3 * W || bgr_pitch < 3 * W || gray_pitch < W || !al4(work) ||
+        (parity != 0 && parity != 1) || (long long)W * H > (1LL << 24))
+        return USV_ERR_INVALID_ARG;
+    uint32_t* wL = static_cast<uint32_t*>(work);
+    uint32_t* wR = wL + USV_FRAME_PREP_WORK_BYTES / 4;
+    const int vh = al4(bgrL) && al4(bgrR) && al4(hsvL) && al4(hsvR) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
+    const int ve = al4(hsvL) && al4(hsvR) && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) &&
+                   hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 && gray_pitch % 4 == 0;
+    const int nb = usv::prep_blocks(W, H);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, hsvL, hsv_pitch, wL},
+                       usv::HistJob{bgrR, pitch, hsvR, hsv_pitch, wR}, W, H, parity, nb, vh);
+    if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
+    hipLaunchKernelGGL(usv::equalize_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s,
+                       usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
+                       usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
+    return usv::st(hipGetLastError());
+}
+
+usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                    const int16_t* map1L, const uint16_t* map2L, const int16_t* map1R,
+                                    const uint16_t* map2R, int W, int H, uint8_t* hsvL, uint8_t* hsvR, int hsv_pitch,
+                                    uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch, uint8_t* grayL,
+                                    uint8_t* grayR, int gray_pitch, void* work, int parity, void* stream) {
+    if (!srcL || !srcR || !map1L || !map2L || !map1R || !map2R || !hsvL || !hsvR || !bgr_outL || !bgr_outR ||
+        !grayL || !grayR || !work || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || spitch < 3 * sW ||
+        hsv_pitch < 3 * W || bgr_pitch < 3 * W || gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) ||
+        (long long)W * H > (1LL << 24))
+        return USV_ERR_INVALID_ARG;
+    if ((long long)(sH + 1) * spitch >= (1LL << 32) || spitch >= (1 << 24)) return USV_ERR_UNSUPPORTED;
+    uint32_t* wL = static_cast<uint32_t*>(work);
+    uint32_t* wR = wL + USV_FRAME_PREP_WORK_BYTES / 4;
+    auto al = [](const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
+    const int vec_map = (W % 4) == 0 && al(map1L, 16) && al(map1R, 16) && al(map2L, 8) && al(map2R, 8);
+    const int vec_src = al4(srcL) && al4(srcR) && spitch % 4 == 0 && spitch >= 12;
+    const int vec_hsv = al4(hsvL) && al4(hsvR) && hsv_pitch % 4 == 0;
+    const int ve = vec_hsv && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) && bgr_pitch % 4 == 0 &&
+                   gray_pitch % 4 == 0;
+    // rectify + HSV + histogram: a quad per thread per iteration, ~4 quads per thread at 1080p
+    const long long quads = (long long)((W + 3) / 4) * H;
+    const int per_job = (int)std::max<long long>(1, std::min<long long>(1024, (quads + 1023) / 1024));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const usv::RectPrepJob jl{{srcL, spitch, map1L, map2L, hsvL, hsv_pitch}, wL};
+    const usv::RectPrepJob jr{{srcR, spitch, map1R, map2R, hsvR, hsv_pitch}, wR};
+    hipLaunchKernelGGL(usv::rectify_hsv_hist_kernel, dim3(2 * per_job), dim3(256), 0, s, jl, jr, sW, sH, W, H, per_job,
+                       vec_map, vec_src, vec_hsv, parity);
+    if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
+    const int nb = usv::prep_blocks(W, H);
+    hipLaunchKernelGGL(usv::equalize_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s,
+                       usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
+                       usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
+    return usv::st(hipGetLastError());
 }
 
 usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch, int thresh,

@@ -78,6 +78,76 @@ def frame_prep(bgr: torch.Tensor, stream=None):
     return FramePrep(bgr.device)(bgr, stream=stream)
 
 
+class FramePrepPair:
+    """Both cameras' frame preparation in two launches (usv_frame_prep_pair_u8), or the whole per-frame
+    stage including rectification (usv_rectify_prep_pair_u8, rectify_prep).  Owns one workspace per
+    camera (2 x USV_FRAME_PREP_WORK_BYTES) and alternates its parity per call."""
+
+    def __init__(self, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.work = torch.zeros(2 * FramePrep.WORK_WORDS, dtype=torch.int32, device=dev)
+        self.parity = 0
+
+    def hist(self, camera: int) -> torch.Tensor:
+        """The last frame's 256-bin histogram of V of camera 0 (L) or 1 (R)."""
+        p = 1 - self.parity
+        base = camera * FramePrep.WORK_WORDS
+        return self.work[base + 2048 * p:base + 2048 * (p + 1)].view(8, 256).sum(0)
+
+    @staticmethod
+    def _outs(ref: torch.Tensor, H: int, W: int, outs):
+        if outs is None:
+            outs = [torch.empty((H, W, 3), dtype=torch.uint8, device=ref.device) for _ in range(4)] + \
+                   [torch.empty((H, W), dtype=torch.uint8, device=ref.device) for _ in range(2)]
+        hl, hr, bl, br, gl, gr = outs
+        for t, n in ((hl, "hsvL"), (hr, "hsvR"), (bl, "bgrL"), (br, "bgrR")):
+            _u8(t, n, 3)
+        _u8(gl, "grayL", 1)
+        _u8(gr, "grayR", 1)
+        if hl.stride() != hr.stride() or bl.stride() != br.stride() or gl.stride() != gr.stride():
+            raise ValueError("the two cameras' outputs must share their row pitches")
+        return outs
+
+    def __call__(self, bgr_l: torch.Tensor, bgr_r: torch.Tensor, outs=None, stream=None):
+        """((hsv'_L, hsv'_R), (bgr'_L, bgr'_R), (gray_L, gray_R)) of a rectified BGR pair."""
+        _u8(bgr_l, "bgr_l", 3)
+        _u8(bgr_r, "bgr_r", 3)
+        if bgr_l.shape != bgr_r.shape or bgr_l.stride() != bgr_r.stride():
+            raise ValueError("the two frames must share shape and strides")
+        H, W = bgr_l.shape[:2]
+        hl, hr, bl, br, gl, gr = self._outs(bgr_l, H, W, outs)
+        lib = _lib.load()
+        with torch.cuda.device(bgr_l.device):
+            _lib.check("usv_frame_prep_pair_u8", lib.usv_frame_prep_pair_u8(
+                bgr_l.data_ptr(), bgr_r.data_ptr(), W, H, bgr_l.stride(0), hl.data_ptr(), hr.data_ptr(),
+                hl.stride(0), bl.data_ptr(), br.data_ptr(), bl.stride(0), gl.data_ptr(), gr.data_ptr(),
+                gl.stride(0), self.work.data_ptr(), self.parity, _stream(stream)))
+        self.parity ^= 1
+        return (hl, hr), (bl, br), (gl, gr)
+
+    def rectify_prep(self, left, right, src_l: torch.Tensor, src_r: torch.Tensor, outs=None, stream=None):
+        """The same outputs from the RAW BGR frames and the two cameras' Rectifier maps, in two launches
+        (rectification fused into the HSV + histogram pass; no rectified-BGR intermediate)."""
+        _u8(src_l, "src_l", 3)
+        _u8(src_r, "src_r", 3)
+        if src_l.shape != src_r.shape or src_l.stride() != src_r.stride():
+            raise ValueError("the two frames must share shape and strides")
+        sH, sW = src_l.shape[:2]
+        W, H = left.W, left.H
+        if (right.W, right.H) != (W, H):
+            raise ValueError("the two rectifiers must share the output size")
+        hl, hr, bl, br, gl, gr = self._outs(src_l, H, W, outs)
+        lib = _lib.load()
+        with torch.cuda.device(src_l.device):
+            _lib.check("usv_rectify_prep_pair_u8", lib.usv_rectify_prep_pair_u8(
+                src_l.data_ptr(), src_r.data_ptr(), sW, sH, src_l.stride(0), left.map1.data_ptr(),
+                left.map2.data_ptr(), right.map1.data_ptr(), right.map2.data_ptr(), W, H, hl.data_ptr(),
+                hr.data_ptr(), hl.stride(0), bl.data_ptr(), br.data_ptr(), bl.stride(0), gl.data_ptr(),
+                gr.data_ptr(), gl.stride(0), self.work.data_ptr(), self.parity, _stream(stream)))
+        self.parity ^= 1
+        return (hl, hr), (bl, br), (gl, gr)
+
+
 def ABSDiffSearch(gray: torch.Tensor, prev: torch.Tensor | None, thresh: int = 40,
                   out: torch.Tensor | None = None, stream=None):
     """Motion mask of P/Main.cpp:299-312.  Returns (mask, next_prev): as in the
