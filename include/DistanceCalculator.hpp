@@ -3,7 +3,7 @@
 // Same declarations, macro values and namespace leaks (using namespace cv /
 // std / std::chrono, P/DistanceCalculator.hpp:12-14), so the reference's
 // Main.cpp compiles against it unchanged.  The implementation lives in
-// libusv.so (csrc/host/DistanceCalculator.cpp), built with -ffp-contract=off.
+// libusv.so (csrc/host/distance_calculator.cpp), built with -ffp-contract=off.
 #ifndef DistanceCalculator_HPP
 #define DistanceCalculator_HPP
 

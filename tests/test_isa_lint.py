@@ -25,14 +25,22 @@ def _disassembly(tmp_path):
     if not shutil.which("objcopy") or not os.path.exists(f"{LLVM}/llvm-objdump"):
         pytest.skip("objcopy / llvm-objdump not available")
     fat = tmp_path / "fat.bin"
-    co = tmp_path / "gfx950.co"
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", _lib.LIB_PATH, str(fat)],
                    check=True)
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"],
-                   check=True)
-    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", str(co)], check=True,
-                         capture_output=True, text=True).stdout
+    # the section holds one offload bundle per translation unit: unbundle each one's gfx950 object
+    data = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = ""
+    for n, a in enumerate(starts):
+        b = starts[n + 1] if n + 1 < len(starts) else len(data)
+        part, co = tmp_path / f"bundle{n}.bin", tmp_path / f"gfx950_{n}.co"
+        part.write_bytes(data[a:b])
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}", f"--output={co}"],
+                       check=True)
+        out += subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", str(co)], check=True,
+                              capture_output=True, text=True).stdout
     funcs, cur = {}, None
     for line in out.splitlines():
         m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
@@ -158,3 +166,32 @@ def test_lds_dma_m0_wait_state(fast_kernels):
         for a, b in zip(ins, ins[1:]):
             if b.startswith("global_load_lds") or (b.startswith("buffer_load") and b.endswith(" lds")):
                 assert not re.match(r"s_\w+ m0,", a), (name, a, b)
+
+
+@pytest.fixture(scope="module")
+def tiled_kernels(tmp_path_factory):
+    funcs = _disassembly(tmp_path_factory.mktemp("isa_tiled"))
+    tiled = {k: v for k, v in funcs.items() if "sad_tiled_kernel" in k}
+    assert len(tiled) >= 2, sorted(tiled)  # SAD and SSD, every radius the dispatch instantiates
+    return tiled
+
+
+def test_tiled_no_scratch(tiled_kernels):
+    bad = {k: sum("scratch_" in i for i in v) for k, v in tiled_kernels.items()}
+    assert not any(bad.values()), {k: n for k, n in bad.items() if n}
+
+
+def test_tiled_lds_dma_m0_wait_state(tiled_kernels):
+    # the tiled kernel's ring (csrc/usv_sad_tiled.hip tdma) writes M0 in inline asm too
+    n_dma = 0
+    for name, ins in tiled_kernels.items():
+        for a, b in zip(ins, ins[1:]):
+            if b.startswith("global_load_lds") or (b.startswith("buffer_load") and b.endswith(" lds")):
+                n_dma += 1
+                assert not re.match(r"s_\w+ m0,", a), (name, a, b)
+    assert n_dma > 0
+
+
+def test_tiled_no_sgpr_use_while_scalar_load_in_flight(tiled_kernels):
+    bad = {k: inflight_scalar_load_hazards(v)[:3] for k, v in tiled_kernels.items()}
+    assert not any(bad.values()), {k: v for k, v in bad.items() if v}

@@ -4,8 +4,8 @@
 // P/DistanceCalculator.hpp:30-48) plus the per-disparity distance table used
 // by the GPU path.  MUST be compiled with -ffp-contract=off: the extrapolated
 // centroid feeds an (int) truncation, and an FMA-contracted build changes it
-// (SURVEY.md §0.7).  Parity: tests/test_distance_parity.py (vs the oracle and
-// the SURVEY.md §8(c) golden values).
+// (SURVEY.md §0.7).  Parity: tests/test_capi.py and tests/test_cpp_api.py (vs
+// oracle/distance_oracle.c) and tests/test_oracle.py (the SURVEY.md §8(c) golden values).
 #include "DistanceCalculator.hpp"
 
 #include <cmath>
