@@ -71,14 +71,21 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
 // remap_quad (usv_remap.hpp) computes it, the result leaves as one 4-B (gray) or one 12-B (BGR)
 // store.  (Two or four quads per thread with every load issued first ran slower: 18.1 / 24.6 us
 // vs 15.1 us for the 1080p BGR pair on one box.)
+#ifndef USV_REMAP_BLOCK
+#define USV_REMAP_BLOCK 256  // threads per block
+#endif
+#ifndef USV_REMAP_XCD
+#define USV_REMAP_XCD 1  // XCD-contiguous block order
+#endif
+constexpr int kRemapBlock = USV_REMAP_BLOCK;
 template <int CN>
-__global__ __launch_bounds__(256) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
+__global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
                                                     unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
-    const unsigned lb = xcd_block(blockIdx.x, gridDim.x);
+    const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const unsigned job = lb >= blocks_per_job ? 1u : 0u;
     const RemapJob& j = job ? j1 : j0;
     const unsigned nq = (unsigned)(W + 3) >> 2;
-    const unsigned q = (lb - job * blocks_per_job) * 256u + threadIdx.x;
+    const unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
     if (q >= nq * (unsigned)H) return;
     const int y = (int)(q / nq);
     const int x0 = 4 * (int)(q - (unsigned)y * nq);
@@ -117,10 +124,10 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
         a.spitch >= (1 << 24) || b.spitch >= (1 << 24))
         return USV_ERR_UNSUPPORTED;
     const long long quads = (long long)((W + 3) / 4) * H;
-    const long long per_job = (quads + 255) / 256;
+    const long long per_job = (quads + kRemapBlock - 1) / kRemapBlock;
     if (a.spitch < 4 * (cn == 1 ? 2 : 3) || b.spitch < 4 * (cn == 1 ? 2 : 3)) vec_src = false;  // rows too short for the aligned reads
     if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
-    dim3 grid((unsigned)(per_job * n_jobs)), block(256);
+    dim3 grid((unsigned)(per_job * n_jobs)), block(kRemapBlock);
     if (cn == 1)
         hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map,
                            (int)vec_dst, (int)vec_src);

@@ -8,6 +8,10 @@
 #include <cstddef>
 #include <cstdint>
 
+#ifndef USV_REMAP_NT
+#define USV_REMAP_NT 0
+#endif
+
 namespace usv {
 
 struct RemapJob {
@@ -50,8 +54,17 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
     int mx[4], my[4], mf[4];
     const size_t mrow = (size_t)y * W + x0;
     if (vec_map && n == 4) {
+#if USV_REMAP_NT  // the maps are read once per frame: non-temporal loads
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        const v4i av = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(j.map1 + 2 * mrow));
+        const v2u fv = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(j.map2 + mrow));
+        const int4 a = make_int4(av[0], av[1], av[2], av[3]);
+        const uint2 f = make_uint2(fv[0], fv[1]);
+#else
         const int4 a = *reinterpret_cast<const int4*>(j.map1 + 2 * mrow);
         const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
+#endif
         const int w4[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
