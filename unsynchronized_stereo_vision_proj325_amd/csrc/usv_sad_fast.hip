@@ -138,7 +138,7 @@ struct LSeg {
                                  : (LOFF + j < LOFF + K + RAD - 1 ? LOFF + j : LOFF + K + RAD - 1);
     }
     static_assert(EDGE != kRight || (LOFF + K + RAD) % 4 == 0, "right segment ends on a dword");
-    static_assert(NLD == 4 || NLD == 5 || NLD == 6 || NLD == 8, "scalar segment is 4, 5, 6 or 8 dwords");
+    static_assert(NLD >= 4 && NLD <= 8 && (NLD != 7 || K == 12), "scalar segment is 4, 5, 6 or 8 dwords (7: K = 12, loaded as 8)");
 };
 
 // An L byte that sits at byte 0 of its dword is used as the whole dword: the
@@ -1107,9 +1107,12 @@ struct PCfg {
 // destination into other SGPRs before the wait (seen at loop latches), reading stale words.
 template <int N>
 __device__ __forceinline__ typename SWords<N>::T s_load_words_pin(const uint8_t* p, uint32_t off) {
-    static_assert(N == 4 || N == 6 || N == 8, "paired kernel segments are 4, 6 or 8 dwords");
+    static_assert(N == 4 || N == 5 || N == 6 || N == 8, "paired kernel segments are 4, 5, 6 or 8 dwords");
     typename SWords<N>::T w;
-    if constexpr (N == 4)
+    if constexpr (N == 5)
+        asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dword %1, %2, %3 offset:0x10"
+                     : "=&{s[40:43]}"(w.a), "=&{s44}"(w.b) : "s"(p), "s"(off) : "memory");
+    else if constexpr (N == 4)
         asm volatile("s_load_dwordx4 %0, %1, %2" : "=&{s[40:43]}"(w) : "s"(p), "s"(off) : "memory");
     else if constexpr (N == 8)
         asm volatile("s_load_dwordx8 %0, %1, %2" : "=&{s[40:47]}"(w) : "s"(p), "s"(off) : "memory");
@@ -1121,6 +1124,7 @@ __device__ __forceinline__ typename SWords<N>::T s_load_words_pin(const uint8_t*
 template <int N>
 __device__ __forceinline__ void wait_lgkm0_pin(typename SWords<N>::T& w) {
     if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:43]}"(w) : : "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:43]}"(w.a), "+{s44}"(w.b) : : "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:47]}"(w) : : "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[40:43]}"(w.a), "+{s[44:45]}"(w.b) : : "memory");
 }
@@ -1670,9 +1674,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 //     the rotated order (j + p) & 3; each word gives two keys (cost << 8) | d by v_perm, folded
 //     into one accumulator with v_min3; two quad DPP rounds finish.  The 18 pieces ride on the
 //     next row's chain steps (pipelined as in the K = 8 r = 5 kernel).
-template <int RAD>
+template <int RAD, int KK>
 struct P16Cfg {
-    static constexpr int K = 16;
+    static constexpr int K = KK;
+    static constexpr int KS = 16;                       // comb slots per row (pixel slots of the transpose)
     static constexpr int WIN = 2 * RAD + 1;
     static constexpr int NPOS = K + 2 * RAD;            // chain steps
     static constexpr int NE = NPOS + 1;                 // staged entries a lane reads per row
@@ -1688,9 +1693,10 @@ struct P16Cfg {
     static constexpr int TB_OFF = RBUF_OFF + NB * NRS;
     static constexpr int TB_WORDS = K * 64;
     static constexpr int COMB_OFF = TB_OFF + TB_WORDS;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * K;
+    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * KS;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
-    static_assert(RAD == 5, "K = 16 paired kernel: w = 11");
+    static_assert(RAD == 5, "K = 12 / 16 paired kernel: w = 11");
+    static_assert(K == 12 || K == 16, "12 or 16 columns per lane");
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
 };
@@ -1701,15 +1707,17 @@ struct P16Cfg {
 #define USV_P16_EBATCH 4  // vector reads (2 entries each) in the first batch of a row's staged entries
 #endif
 
-template <int RAD, int EDGE>
+template <int RAD, int KK, int EDGE>
 __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                  uint8_t* __restrict__ disp, double* __restrict__ dist,
                                                  const MatchArgs& a, uint32_t* smem, int lane, int x0, int y_begin,
                                                  int y_end) {
-    using C = P16Cfg<RAD>;
+    using C = P16Cfg<RAD, KK>;
     using LS = LSeg<RAD, EDGE, C::K>;
-    using LWords = typename SWords<LS::NLD>::T;
-    constexpr int WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
+    // (K = 12 interior tiles need 7 dwords: load 8, still inside the row since x0 <= W - 2K)
+    constexpr int NLD = LS::NLD == 7 ? 8 : LS::NLD;
+    using LWords = typename SWords<NLD>::T;
+    constexpr int WIN = C::WIN, K = C::K, KS = C::KS, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
     constexpr int NDMA = C::NQ;
     const int lmax = min(63, a.D / 2 - 1);
     const int l_eff = min(lane, lmax);
@@ -1756,7 +1764,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
     };
     LWords lw_next;
-    auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
+    auto load_lw = [&](int t) { lw_next = s_load_words_pin<NLD>(Lseg, row_off(t)); };
     using VT = typename VecT<C::VEC>::T;
     constexpr int NV = C::NE_V / C::VEC;
     constexpr int NV1 = USV_P16_EBATCH < NV ? USV_P16_EBATCH : NV;
@@ -1784,10 +1792,10 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         }
         uint32_t Lv[NPOS];
         {
-            wait_lgkm0_pin<LS::NLD>(lw_next);
+            wait_lgkm0_pin<NLD>(lw_next);
             LWords cur = lw_next;
             uint32_t lw[8];
-            unpack_words<LS::NLD>(cur, lw);
+            unpack_words<NLD>(cur, lw);
 #pragma unroll
             for (int j = 0; j < NPOS; ++j) {
                 const int bidx = LS::byte(j);
@@ -1843,7 +1851,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         } else {
             int rl = rawL;
             asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            lw_next = s_load_words_pin<NLD>(Lseg, (uint32_t)min(rl, last_off));
             rawL = rl + a.pitch;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1855,23 +1863,25 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const uint32_t* crow = comb + (cb * KRB) * K;
+        const uint32_t* crow = comb + (cb * KRB) * KS;
         if (wide) {
-            if (tid < rows) {  // lane r: row r's 16 disparity bytes (byte 0 of each key), one 16-B store
-                const uint4* kr = reinterpret_cast<const uint4*>(crow + tid * K);
-                uint32_t o[4];
+            if (tid < rows) {  // lane r: row r's K disparity bytes (byte 0 of each key), one store
+                const uint4* kr = reinterpret_cast<const uint4*>(crow + tid * KS);
+                uint32_t o[K / 4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < K / 4; ++i) {
                     const uint4 k = kr[i];
                     o[i] = __builtin_amdgcn_perm(k.y, k.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k.w, k.z, 0x04000c0cu);
+                    asm volatile("" ::: "memory");  // one 16-B window live at a time
                 }
-                *reinterpret_cast<uint4*>(disp + (size_t)(y_chunk + tid) * a.disp_pitch + x0) =
-                    make_uint4(o[0], o[1], o[2], o[3]);
+                uint8_t* dp = disp + (size_t)(y_chunk + tid) * a.disp_pitch + x0;
+                if constexpr (K == 16) *reinterpret_cast<uint4*>(dp) = make_uint4(o[0], o[1], o[2], o[3]);
+                else *reinterpret_cast<uint3*>(dp) = make_uint3(o[0], o[1], o[2]);
             }
-            if (dist && tid < 4 * rows) {  // lane 4r + q: distances 4q .. 4q + 3 of row r
+            if (dist && tid < (K / 4) * rows) {  // lane (K/4) r + q: distances 4q .. 4q + 3 of row r
                 struct __attribute__((aligned(8))) D2 { double a, b; };
-                const int r = tid >> 2, q = tid & 3;
-                const uint4 k = reinterpret_cast<const uint4*>(crow + r * K)[q];
+                const int r = tid / (K / 4), q = tid - r * (K / 4);
+                const uint4 k = reinterpret_cast<const uint4*>(crow + r * KS)[q];
                 double* o = dist + (size_t)(y_chunk + r) * a.dist_pitch + x0 + 4 * q;
                 reinterpret_cast<D2*>(o)[0] = D2{lut_s[k.x & 0xFFu], lut_s[k.y & 0xFFu]};
                 reinterpret_cast<D2*>(o)[1] = D2{lut_s[k.z & 0xFFu], lut_s[k.w & 0xFFu]};
@@ -1879,7 +1889,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         } else {
             for (int i = tid; i < rows * K; i += 64) {
                 const int row = i / K, px = i - row * K;
-                const uint32_t dv = crow[row * K + px] & 0xFFu;
+                const uint32_t dv = crow[row * KS + px] & 0xFFu;
                 const size_t y = (size_t)(y_chunk + row);
                 disp[y * a.disp_pitch + x0 + px] = (uint8_t)dv;
                 if (dist) dist[y * a.dist_pitch + x0 + px] = lut_s[dv];
@@ -1921,7 +1931,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             acc = min(acc, dpp<kQuadSwap1>(acc));
         } else if constexpr (J == 17) {
             acc = min(acc, dpp<kQuadSwap2>(acc));
-            comb[(cb * KRB + slot) * K + tp] = acc;
+            comb[(cb * KRB + slot) * KS + tp] = acc;  // pixel slots >= K (K = 12) are padding
         }
     };
     auto tr_finish = [&](int slot) {
@@ -1958,7 +1968,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
         }(std::make_integer_sequence<int, WIN>{});
     }
-    wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
+    wait_lgkm0_pin<NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
     {
         const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
         tr_finish(last);
@@ -1972,13 +1982,13 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
 #ifndef USV_P16_OCC
 #define USV_P16_OCC 2  // waves per SIMD the K = 16 paired kernel is compiled for
 #endif
-template <int RAD>
+template <int RAD, int KK>
 __global__ __launch_bounds__(64, USV_P16_OCC) void sad_pair16_kernel(const uint8_t* __restrict__ L,
                                                                      const uint8_t* __restrict__ R,
                                                                      uint8_t* __restrict__ disp,
                                                                      double* __restrict__ dist, MatchArgs a,
                                                                      BandPlan P) {
-    using C = P16Cfg<RAD>;
+    using C = P16Cfg<RAD, KK>;
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
     const unsigned total = gridDim.x, lin = blockIdx.x;
@@ -2021,11 +2031,11 @@ __global__ __launch_bounds__(64, USV_P16_OCC) void sad_pair16_kernel(const uint8
     __syncthreads();
     if (y_end <= y_begin) return;
     if (xt == 0)
-        pair16_band_loop<RAD, kLeft>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+        pair16_band_loop<RAD, KK, kLeft>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
     else if (xt == n_xt - 1)
-        pair16_band_loop<RAD, kRight>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+        pair16_band_loop<RAD, KK, kRight>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
     else
-        pair16_band_loop<RAD, kInterior>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+        pair16_band_loop<RAD, KK, kInterior>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
 }
 
 #ifndef USV_PAIR_OCC7
@@ -2158,23 +2168,23 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int RAD>
+template <int RAD, int KK>
 int resident_p16_blocks_per_cu() {
     static const int n = [] {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair16_kernel<RAD>, 64, 0) != hipSuccess || v <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair16_kernel<RAD, KK>, 64, 0) != hipSuccess || v <= 0)
             v = 1;
         return v;
     }();
     return n;
 }
 
-template <int RAD>
+template <int RAD, int KK>
 hipError_t launch_pair16_r(const MatchArgs& a, hipStream_t s) {
-    constexpr int K = P16Cfg<RAD>::K, WIN = 2 * RAD + 1;
+    constexpr int K = P16Cfg<RAD, KK>::K, WIN = 2 * RAD + 1;
     BandPlan P{};
     P.n_xt = (a.W + K - 1) / K;
-    const int per_cu = resident_p16_blocks_per_cu<RAD>();
+    const int per_cu = resident_p16_blocks_per_cu<RAD, KK>();
     const long slots = (long)cu_count() * per_cu;
     const long NC = (long)P.n_xt * a.batch;
     long m = slots / NC;
@@ -2193,12 +2203,12 @@ hipError_t launch_pair16_r(const MatchArgs& a, hipStream_t s) {
 #define USV_P16_WEIGHTS 0x01010101u  // band heights by dispatch generation (equal: not fitted yet)
 #endif
     P.weights = per_cu == 8 && total > 2L * 8 * P.gen_g ? USV_P16_WEIGHTS : 0x01010101u;
-    hipLaunchKernelGGL((sad_pair16_kernel<RAD>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a, P);
+    hipLaunchKernelGGL((sad_pair16_kernel<RAD, KK>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
 }
 
 #ifndef USV_PAIR16
-#define USV_PAIR16 0  // K = 16 paired kernel for w = 11, even 64 < D <= 128
+#define USV_PAIR16 0  // 12 or 16: the wide paired kernel with that many columns per lane (w = 11, even 64 < D <= 128); 0 = off
 #endif
 #ifndef USV_PAIR
 #define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
@@ -2251,11 +2261,11 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
     return launch_rn<USV_DEV_ONLY_RAD, USV_DEV_ONLY_NW>(a, s);
 #elif defined(USV_EXP_PAIR_ONLY)  // timing experiments: the paired kernel only (configs C and E)
     if (!pair_path_supported(a)) return hipErrorInvalidValue;
-    if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5>(a, s);
+    if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
     return a.w == 11 ? launch_pair_r<5>(a, s) : a.w == 15 ? launch_pair_r<7>(a, s) : hipErrorInvalidValue;
 #else
     if (pair_path_supported(a)) {
-        if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5>(a, s);
+        if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
         switch ((a.w - 1) / 2) {
             case 5: return launch_pair_r<5>(a, s);
             case 6: return launch_pair_r<6>(a, s);
