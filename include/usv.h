@@ -149,6 +149,9 @@ typedef struct usv_sharded_engine usv_sharded_engine;
 
 /* HOST: shard [*first, *first + *count) of a batch of `batch` pairs for GPU k of n. */
 usv_status usv_shard_range(int batch, int n_devices, int k, int* first, int* count);
+/* HOST: where pair `pair` of the batch lands in the root's gather buffer, in units of frames:
+ * GPU k's shard starts at slot k * per (per = ceil(max_pairs / n) of the engine). */
+usv_status usv_shard_slot(int batch, int n_devices, int per, int pair, long long* slot);
 
 /* Engine for up to max_pairs W x H pairs per call on the n_devices listed GPUs
  * (distinct HIP ordinals; devices[0] is the gather root).  Allocates each GPU's
@@ -158,11 +161,12 @@ usv_status usv_sharded_create(const int* devices, int n_devices, int max_pairs, 
                               int metric, usv_sharded_engine** out);
 usv_status usv_sharded_destroy(usv_sharded_engine* e);
 
-/* DEVICE buffers of GPU k's shard inputs (dense, pitch W, pair j at j*W*H):
- * fill them and pass L = R = NULL to usv_batch_sharded to match HBM-resident frames. */
+/* DEVICE buffers of GPU k's shard inputs for the NEXT submit (dense, pitch W, pair j at j*W*H;
+ * the engine alternates two buffer slots per GPU): fill them and pass L = R = NULL to
+ * usv_batch_sharded(_submit) to match HBM-resident frames. */
 usv_status usv_sharded_input_buffers(usv_sharded_engine* e, int k, uint8_t** L, uint8_t** R);
 
-/* DEVICE results on devices[0] after usv_batch_sharded: the gather buffer
+/* DEVICE results on devices[0] of the last COMPLETED batch: the gather buffer
  * (GPU k's shard at slot k, i.e. k * ceil(max_pairs / n) * W * H bytes; equal
  * to batch order when batch == n * ceil(max_pairs / n)) and the distance maps
  * in batch order (NULL until a call asked for them). */
@@ -180,6 +184,15 @@ usv_status usv_sharded_outputs(usv_sharded_engine* e, const uint8_t** disp, cons
 usv_status usv_batch_sharded(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int batch,
                              size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
                              const double* lut_cm, int with_distance);
+/* The same in two halves, two batches in flight: submit enqueues a batch on the next of two buffer
+ * slots (host inputs are read before it returns; a submit while both slots are busy first completes
+ * the older batch) and returns *ticket; wait completes that batch (disp / dist_cm filled).  Batch
+ * k+1's copies and kernels overlap batch k's gather, distance expansion and D2H.  The host output
+ * buffers of a batch must stay valid until its wait. */
+usv_status usv_batch_sharded_submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int batch,
+                                    size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
+                                    const double* lut_cm, int with_distance, long long* ticket);
+usv_status usv_batch_sharded_wait(usv_sharded_engine* e, long long ticket);
 
 /* ---- streaming host frames (the reference's caller hands over HOST frames per camera
  * thread, P/Main.cpp:876-921, 1238-1242) ----

@@ -105,3 +105,53 @@ def _copy_from_device(ptr, n):
     out = np.empty(n, np.uint8)
     assert lib.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), ctypes.c_size_t(n), 2) == 0
     return out
+
+
+def test_shard_slot_mapping(usvlib):
+    """usv_shard_slot: pair -> gather slot of the root buffer (GPU k's shard at k * per), for ragged
+    batches and n = 1..8 -- injective, inside [0, n * per), contiguous and ordered within a shard."""
+    slot = ctypes.c_longlong()
+    first, count = ctypes.c_int(), ctypes.c_int()
+    for n in range(1, 9):
+        for max_pairs in (n, n + 1, 2 * n + 3, 17):
+            per = (max_pairs + n - 1) // n
+            for batch in range(1, max_pairs + 1):
+                seen = []
+                for p in range(batch):
+                    assert usvlib.usv_shard_slot(batch, n, per, p, ctypes.byref(slot)) == _lib.USV_OK
+                    seen.append(slot.value)
+                assert len(set(seen)) == batch and all(0 <= v < n * per for v in seen)
+                for k in range(n):
+                    usvlib.usv_shard_range(batch, n, k, ctypes.byref(first), ctypes.byref(count))
+                    got = seen[first.value:first.value + count.value]
+                    assert got == list(range(k * per, k * per + count.value)), (n, batch, k)
+    assert usvlib.usv_shard_slot(4, 2, 1, 0, ctypes.byref(slot)) == _lib.USV_ERR_INVALID_ARG  # per too small
+    assert usvlib.usv_shard_slot(4, 2, 2, 4, ctypes.byref(slot)) == _lib.USV_ERR_INVALID_ARG  # pair past batch
+
+
+@pytest.mark.gpu
+def test_batch_sharded_two_batches_in_flight(gpu):
+    """submit / wait with two batches in flight on the engine's two buffer slots (and a third submit that
+    first completes the oldest): every batch bit-exact vs the oracle, distances on the root."""
+    W, H, D, w = 640, 480, 64, 7
+    batches = [[synthetic_pair(W, H, D, pair_index=80 + 3 * b + i, noise=2)[:2] for i in range(3 - (b % 2))]
+               for b in range(3)]
+    eng = ShardedMatcher([0], 3, W, H, D, w)
+    try:
+        hs = [eng.submit(np.stack([p[0] for p in bt]), np.stack([p[1] for p in bt]), with_distance=(b == 1))
+              for b, bt in enumerate(batches)]
+        lut = distance_lut_cm()
+        for b, (h, bt) in enumerate(zip(hs, batches)):
+            if b == 0:
+                # the third submit reused batch 0's slot: it completed batch 0 itself, so its ticket is gone
+                with pytest.raises(_lib.UsvError):
+                    eng.wait(h)
+                disp = h["disp"]
+            else:
+                disp, dist = eng.wait(h)
+                if b == 1:
+                    assert np.array_equal(dist[~np.isinf(dist)], lut[disp][~np.isinf(dist)])
+            for i, (l, r) in enumerate(bt):
+                assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), (b, i)
+    finally:
+        eng.close()

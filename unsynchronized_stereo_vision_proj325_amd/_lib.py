@@ -75,6 +75,10 @@ SIGNATURES = {
                                         c_int, c_int, c_int, c_void_p, c_size_t, c_int, c_void_p,
                                         c_size_t, c_int, c_void_p, c_void_p]),
     "usv_shard_range": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
+    "usv_shard_slot": (c_int, [c_int, c_int, c_int, c_int, POINTER(ctypes.c_longlong)]),
+    "usv_batch_sharded_submit": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_size_t, c_int, c_void_p, c_void_p,
+                                         c_void_p, c_int, POINTER(ctypes.c_longlong)]),
+    "usv_batch_sharded_wait": (c_int, [c_void_p, ctypes.c_longlong]),
     "usv_sharded_create": (c_int, [POINTER(c_int), c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                    POINTER(c_void_p)]),
     "usv_sharded_destroy": (c_int, [c_void_p]),

@@ -194,3 +194,32 @@ class ShardedMatcher:
             self.handle, vp(L), vp(R), batch, self.H * self.W, self.W, vp(disp), vp(dist), vp(lut_arr),
             int(bool(with_distance))))
         return disp, dist
+
+    def submit(self, L, R, with_distance: bool = False, lut=None):
+        """Enqueue a host batch on the engine's next buffer slot (usv_batch_sharded_submit) and return a
+        handle for wait(); two batches can be in flight."""
+        import numpy as np
+        ct = self._ct
+        L = np.ascontiguousarray(L)
+        R = np.ascontiguousarray(R)
+        if L.shape != R.shape or L.ndim != 3 or L.shape[1:] != (self.H, self.W) or L.dtype != np.uint8:
+            raise ValueError("L, R must be (B, H, W) uint8 batches of the engine's geometry")
+        batch = L.shape[0]
+        disp = np.empty((batch, self.H, self.W), np.uint8)
+        dist = np.empty((batch, self.H, self.W), np.float64) if with_distance else None
+        if with_distance and lut is None:
+            from .engine import distance_lut_cm
+            lut = distance_lut_cm()
+        lut_arr = np.ascontiguousarray(lut, dtype=np.float64) if lut is not None else None
+        vp = lambda a: a.ctypes.data_as(ct.c_void_p) if a is not None else None  # noqa: E731
+        t = ct.c_longlong()
+        self._lib_mod.check("usv_batch_sharded_submit", self.lib.usv_batch_sharded_submit(
+            self.handle, vp(L), vp(R), batch, self.H * self.W, self.W, vp(disp), vp(dist), vp(lut_arr),
+            int(bool(with_distance)), ct.byref(t)))
+        # the host outputs (and the table) must outlive the batch: keep them with the ticket
+        return {"ticket": t.value, "disp": disp, "dist": dist, "keep": (L, R, lut_arr)}
+
+    def wait(self, h):
+        """Complete a submitted batch: (disp, dist or None) in batch order."""
+        self._lib_mod.check("usv_batch_sharded_wait", self.lib.usv_batch_sharded_wait(self.handle, h["ticket"]))
+        return h["disp"], h["dist"]
