@@ -233,8 +233,10 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
 
 
 def spawn_ranks(n: int, need_gpus: bool) -> int:
-    """Run this script as N ranks under torch.distributed.run (a child process; this process has not
-    touched the GPU: torch.cuda.device_count() does not initialise it) and return its exit status."""
+    """Run this script as N ranks under torch.distributed.run and return its exit status.  The
+    launcher is a fresh child process (subprocess, never an exec of this one), so it is legal even
+    if torch.cuda.device_count() initialised the HIP runtime here (it may: without amdsmi PyTorch
+    counts with hipGetDeviceCount); each rank re-checks WORLD_SIZE against the GPUs it sees."""
     import socket
     import subprocess
     if need_gpus:
@@ -588,10 +590,11 @@ def matcher_leg(dev, n: int = 150, max_pts: int = 120, runs: int = 5) -> dict:
 
 
 def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> dict:
-    """What the AUTO dispatch costs off the fast SAD kernels: the tiled sliding-window kernel
-    (csrc/usv_sad_tiled.hip) for SSD at the headline config and for SAD on a 1918-wide (W % 4 != 0)
-    crop of the same pair, and the direct-window generic kernel (csrc/usv_sad_generic.hip,
-    O(D w^2) per pixel, what AUTO ran for these shapes before the tiled kernel) beside them."""
+    """SSD and the paths off the fast SAD kernels: the SSD kernel (csrc/usv_sad_fast.hip
+    ssd_fast_kernel, what AUTO runs for SSD at 11 <= w <= 15) at the headline config; the tiled
+    sliding-window kernel (csrc/usv_sad_tiled.hip) for the same SSD and for SAD on a 1918-wide
+    (W % 4 != 0) crop of the same pair; the direct-window generic kernel (csrc/usv_sad_generic.hip,
+    O(D w^2) per pixel) beside them."""
     s = torch.cuda.current_stream()
     Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
     out = {}
@@ -599,6 +602,9 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     d1 = torch.empty_like(Lt)
     d2 = torch.empty((H, 1918), dtype=torch.uint8, device=dev)
     Lc, Rc = Lt[:, :1918], Rt[:, :1918]
+    ssd = StereoBlockMatcher(D, w, "ssd", kernel="fast")
+    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s)
+    out["ssd_fast"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
     for kernel, n in (("tiled", steps * 8), ("generic", steps)):
         ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)
         us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s)
@@ -607,9 +613,9 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
         us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s)
         out[f"sad_{kernel}_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
                                       "value": 1918 * H / (us * 1e-6)}
-    out["note"] = "AUTO runs the tiled kernel (vertical running sums, LDS-DMA row ring) for SSD and for shapes " \
-                  "outside the fast SAD kernels (W % 4, W < 48, unaligned pitch or base); generic = one thread " \
-                  "per pixel, direct window, now only for w > 31"
+    out["note"] = "AUTO runs ssd_fast for SSD at 11 <= w <= 15 and the tiled kernel (vertical running sums, " \
+                  "LDS-DMA row ring) for other SSD windows and for shapes outside the fast kernels (W % 4, W < 48, " \
+                  "unaligned pitch or base); generic = one thread per pixel, direct window, only for w > 31"
     return out
 
 
@@ -631,6 +637,8 @@ def main():
         return
     if rehearse:
         local %= torch.cuda.device_count()
+    elif local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

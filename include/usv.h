@@ -83,8 +83,9 @@ typedef enum {
 } usv_distance_model;
 
 typedef enum {
-    USV_KERNEL_AUTO = 0,    /* fast SAD path when the shape allows it, else tiled, else generic */
-    USV_KERNEL_FAST = 1,    /* lane-per-disparity packed running-sum SAD kernels; UNSUPPORTED if not applicable */
+    USV_KERNEL_AUTO = 0,    /* fast path when the shape allows it, else tiled, else generic */
+    USV_KERNEL_FAST = 1,    /* lane-per-disparity running-sum kernels: SAD (w <= 15), SSD (11 <= w <= 15);
+                               W % 4 == 0, W >= 48, 4-byte aligned bases / pitch; UNSUPPORTED otherwise */
     USV_KERNEL_GENERIC = 2, /* direct-window kernel, any w <= 63, SAD or SSD (reference-speed fallback) */
     USV_KERNEL_TILED = 3    /* sliding-window kernel: SAD or SSD, any W / pitch / alignment, w <= 31 */
 } usv_kernel;

@@ -51,7 +51,7 @@ def test_argument_validation_needs_no_gpu(usvlib):
     assert usvlib.usv_sad_disparity_ex(p, p, 64, 64, 64, 16, 5, 0, p, 64, p, 64, None, 0, None) == \
         _lib.USV_ERR_INVALID_ARG  # distance map without a LUT
     assert usvlib.usv_sad_disparity_ex(p, p, 64, 64, 64, 16, 5, 1, p, 64, None, 0, None, 1, None) == \
-        _lib.USV_ERR_UNSUPPORTED  # SSD forced onto the fast kernel
+        _lib.USV_ERR_UNSUPPORTED  # SSD at w = 5 forced onto the fast kernel (w >= 11 only)
     assert usvlib.usv_disparity_to_distance(p, 0, 4, 4, p, p, 4, None) == _lib.USV_ERR_INVALID_ARG
     # GPU contour matcher: bad sizes / null outputs rejected, empty sets are a no-op (no launch)
     assert usvlib.usv_contour_descriptors(p, p, -1, p, None) == _lib.USV_ERR_INVALID_ARG

@@ -248,6 +248,49 @@ def test_host_lut_through_c_abi(gpu):
     assert np.array_equal(dist.cpu().numpy(), distance_lut_cm()[disp.cpu().numpy()])
 
 
+_VMM_LUT_SCRIPT = r"""
+import ctypes, sys
+import numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from unsynchronized_stereo_vision_proj325_amd import _lib
+from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm
+lib = _lib.load()
+rng = np.random.default_rng(5)
+L = torch.from_numpy(rng.integers(0, 256, (64, 128), dtype=np.uint8)).cuda()
+R = torch.from_numpy(rng.integers(0, 256, (64, 128), dtype=np.uint8)).cuda()
+lut_h = np.ascontiguousarray(distance_lut_cm("canny"))
+lut = torch.from_numpy(lut_h).cuda()          # expandable segment: hipMemCreate / hipMemMap, not hipMalloc
+disp = torch.empty_like(L)
+dist = torch.zeros((64, 128), dtype=torch.float64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+_lib.check("ex", lib.usv_sad_disparity_ex(L.data_ptr(), R.data_ptr(), 128, 64, 128, 32, 5, 0, disp.data_ptr(),
+                                          128, dist.data_ptr(), 128, lut.data_ptr(), 0, s))
+torch.cuda.synchronize()
+assert np.array_equal(dist.cpu().numpy(), lut_h[disp.cpu().numpy()])
+dist.zero_()
+_lib.check("d2d", lib.usv_disparity_to_distance(disp.data_ptr(), 128, 64, 128, lut.data_ptr(), dist.data_ptr(),
+                                                128, s))
+torch.cuda.synchronize()
+assert np.array_equal(dist.cpu().numpy(), lut_h[disp.cpu().numpy()])
+print("ok")
+"""
+
+
+def test_device_lut_from_expandable_segments(gpu):
+    """A device table allocated by PyTorch's expandable-segment allocator (virtual-memory
+    mappings, not hipMalloc) is used in place by the LUT resolution of the C ABI.  Run in a
+    child process: the allocator is chosen before the GPU is initialised."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTORCH_HIP_ALLOC_CONF="expandable_segments:True",
+               PYTORCH_CUDA_ALLOC_CONF="expandable_segments:True")
+    r = subprocess.run([sys.executable, "-c", _VMM_LUT_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_distance_map_mm(gpu):
     """north_star's unit: mm = 10 x cm, fused into the matcher and through the gather kernel."""
     from unsynchronized_stereo_vision_proj325_amd import distance_lut_mm
@@ -292,10 +335,55 @@ def test_disparity_to_distance_kernel(gpu):
             assert (((out == ref) | (np.isinf(out) & np.isinf(ref))).all())
 
 
-def test_fast_kernel_refuses_ssd(gpu):
-    L = torch.zeros((16, 16), dtype=torch.uint8, device=gpu)
-    with pytest.raises(_lib.UsvError):
-        StereoBlockMatcher(8, 5, "ssd", kernel="fast").compute(L, L)
+def test_fast_kernel_refuses_ssd_small_windows(gpu):
+    """The SSD kernel's 8-column L segments exist for 11 <= w <= 15 only."""
+    L = torch.zeros((16, 64), dtype=torch.uint8, device=gpu)
+    for w in (5, 9):
+        with pytest.raises(_lib.UsvError):
+            StereoBlockMatcher(8, w, "ssd", kernel="fast").compute(L, L)
+
+
+def test_ssd_fast_config_c_full_size(gpu):
+    """SSD on the headline shape (1920x1080, 11x11, D = 128) through the SSD kernel, with distances."""
+    L, R, dstar = synthetic_pair(1920, 1080, 128, pair_index=3, noise=2)
+    got, dist = gpu_disp(gpu, L, R, 128, 11, "ssd", kernel="fast", with_distance=True)
+    ref = oracle_sad(L, R, 128, 11, "ssd", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    lut = distance_lut_cm("moving_object")
+    assert np.array_equal(dist, lut[ref])
+
+
+@pytest.mark.parametrize("W,H,D,w", [(48, 40, 1, 11), (52, 37, 64, 11), (60, 29, 65, 13), (100, 50, 128, 15),
+                                     (132, 31, 129, 11), (1916, 23, 256, 13), (64, 16, 256, 15),
+                                     (200, 90, 100, 11), (76, 45, 31, 15)])
+def test_ssd_fast_shapes(gpu, W, H, D, w):
+    """SSD kernel: border tiles (tile 0 replicates column 0, the last tile aligned to W - 8), one, two
+    and four waves per workgroup, bands shorter than the window, ties (low-entropy halves)."""
+    rng = np.random.default_rng(W * 7 + H * 3 + D + w)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    if D % 2:
+        L //= 64
+        R //= 64
+    got = gpu_disp(gpu, L, R, D, w, "ssd", kernel="fast")
+    ref = oracle_sad(L, R, D, w, "ssd", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
+    # AUTO picks the same kernel for these shapes
+    assert np.array_equal(gpu_disp(gpu, L, R, D, w, "ssd"), ref)
+
+
+def test_ssd_fast_max_cost_saturated(gpu):
+    """15x15 window of 0 against 255: the largest SSD (225 x 255^2 = 14.6 M < 2^24) must not wrap the keys."""
+    H, W, D = 40, 96, 64
+    L = np.zeros((H, W), dtype=np.uint8)
+    R = np.full((H, W), 255, dtype=np.uint8)
+    R[:, ::7] = 0  # some cheaper disparities so the argmin is not all-ties
+    got = gpu_disp(gpu, L, R, D, 15, "ssd", kernel="fast")
+    ref = oracle_sad(L, R, D, 15, "ssd", "naive")
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    R[:] = 255
+    got = gpu_disp(gpu, L, R, D, 15, "ssd", kernel="fast")
+    assert np.array_equal(got, oracle_sad(L, R, D, 15, "ssd", "naive"))
 
 
 def test_cpu_tensors_rejected():

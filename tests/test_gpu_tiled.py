@@ -1,6 +1,6 @@
 """GPU parity of the tiled sliding-window kernel (csrc/usv_sad_tiled.hip) vs the CPU oracle.
 
-The tiled kernel is what AUTO runs for SSD and for every shape outside the fast SAD
+The tiled kernel is what AUTO runs for SSD at w < 11 and for every shape outside the fast
 kernels: W % 4 != 0, W < 48, unaligned bases or pitches, w up to 31.  Bit-exact
 against oracle/sad_oracle.c (same border rule, same smallest-d tie rule).
 """
@@ -78,8 +78,9 @@ def test_tiled_unaligned_pitched_views_and_distance(gpu, metric):
     assert np.array_equal(dist.cpu().numpy(), distance_lut_cm()[got])
 
 
-def test_tiled_ssd_batch_auto(gpu):
-    """A batched SSD launch (AUTO routes SSD to the tiled kernel): every pair bit-exact."""
+def test_ssd_batch_auto(gpu):
+    """A batched SSD launch (AUTO takes the SSD kernel at w = 13; batched launches are AUTO only):
+    every pair bit-exact."""
     pairs = [synthetic_pair(1000, 300, 96, pair_index=40 + i, noise=3) for i in range(3)]
     L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
     R = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
