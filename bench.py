@@ -197,7 +197,10 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
 
     rng = np.random.default_rng(7)
     cl, cr = synthetic_calibration(W, H, seed=1)
-    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)  # packed maps (4 B/px)
+    ul, ur = (Rectifier(*cl, (W, H), device=dev, packed=False),
+              Rectifier(*cr, (W, H), device=dev, packed=False))  # OpenCV's map pair (6 B/px)
+    mb = 4 if rl.pmap is not None else 6
     src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     out_l, out_r = torch.empty_like(src_l), torch.empty_like(src_r)
@@ -209,8 +212,10 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
     s = torch.cuda.current_stream()
     px = W * H
     legs = {
-        # 2 cameras x (map 4 + 2 B, source 3 B, output 3 B) per pixel
-        "rectify_pair_bgr": (lambda: rectify_pair(rl, rr, src_l, src_r, out_l, out_r), 2 * px * (6 + 3 + 3)),
+        # 2 cameras x (packed map 4 B, source 3 B, output 3 B) per pixel
+        "rectify_pair_bgr": (lambda: rectify_pair(rl, rr, src_l, src_r, out_l, out_r), 2 * px * (mb + 3 + 3)),
+        # the same through OpenCV's CV_16SC2 + CV_16UC1 map pair (map 4 + 2 B)
+        "rectify_pair_bgr_map_pair": (lambda: rectify_pair(ul, ur, src_l, src_r, out_l, out_r), 2 * px * (6 + 3 + 3)),
         # BGR2HSV+hist (3 in, 3 out) + equalize/HSV2BGR/gray (3 in, 3 + 3 + 1 out), one camera
         "frame_prep": (lambda: prep(out_l, hsv, bgr2, gray), px * (3 + 3 + 3 + 7)),
         # absdiff + threshold + erode + dilate: gray + prev in, mask out
@@ -222,8 +227,9 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
     # both cameras' frame prep in two launches (usv_frame_prep_pair_u8)
     legs["frame_prep_pair"] = (lambda: pair(out_l, out_r, outs=pouts), 2 * px * (3 + 3 + 3 + 7))
     # the whole per-frame stage of the pair in two launches (usv_rectify_prep_pair_u8): rectify + HSV +
-    # histogram (6 map + 3 src + 3 hsv), then equalize / HSV2BGR / gray (3 + 3 + 3 + 1), per camera
-    legs["rectify_prep_pair"] = (lambda: pair.rectify_prep(rl, rr, src_l, src_r, outs=pouts), 2 * px * (12 + 10))
+    # histogram (4 packed map + 3 src + 3 hsv), then equalize / HSV2BGR / gray (3 + 3 + 3 + 1), per camera
+    legs["rectify_prep_pair"] = (lambda: pair.rectify_prep(rl, rr, src_l, src_r, outs=pouts),
+                                 2 * px * (mb + 6 + 10))
     res = {}
     for name, (fn, nbytes) in legs.items():
         us = time_launches(fn, steps, s)
@@ -370,7 +376,10 @@ def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
 
     rng = np.random.default_rng(11)
     cl, cr = synthetic_calibration(W, H, seed=2)
-    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)  # packed maps (4 B/px)
+    ul, ur = (Rectifier(*cl, (W, H), device=dev, packed=False),
+              Rectifier(*cr, (W, H), device=dev, packed=False))  # OpenCV's map pair (6 B/px)
+    mb = 4 if rl.pmap is not None else 6
     src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)
@@ -402,7 +411,10 @@ def frame_chain_fused_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> di
 
     rng = np.random.default_rng(11)
     cl, cr = synthetic_calibration(W, H, seed=2)
-    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)  # packed maps (4 B/px)
+    ul, ur = (Rectifier(*cl, (W, H), device=dev, packed=False),
+              Rectifier(*cr, (W, H), device=dev, packed=False))  # OpenCV's map pair (6 B/px)
+    mb = 4 if rl.pmap is not None else 6
     src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     pair = FramePrepPair(dev)
@@ -440,7 +452,10 @@ def frame_chain_graph_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> di
 
     rng = np.random.default_rng(11)
     cl, cr = synthetic_calibration(W, H, seed=2)
-    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)  # packed maps (4 B/px)
+    ul, ur = (Rectifier(*cl, (W, H), device=dev, packed=False),
+              Rectifier(*cr, (W, H), device=dev, packed=False))  # OpenCV's map pair (6 B/px)
+    mb = 4 if rl.pmap is not None else 6
     src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)

@@ -353,6 +353,22 @@ usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW,
                                const int16_t* map1R, const uint16_t* map2R, int W, int H,
                                uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
 
+/* DEVICE: the map pair above (W x H, for a sW x sH source) packed into ONE uint32 per pixel (4 B
+ * instead of 6; bits 0-9 the fraction index, 10-20 sx + 1, 21-31 sy + 1, a pixel with no tap inside
+ * the source stored as 2047 / 2047).  Sources of at most 2046 x 2046 (USV_ERR_UNSUPPORTED above).
+ * Built once per calibration; remapping through it is bit-identical to remapping through map1/map2
+ * and reads a third fewer map bytes per frame (no reference counterpart: the reference rebuilds its
+ * map every frame, P/Main.cpp:352). */
+usv_status usv_remap_pack_map(const int16_t* map1, const uint16_t* map2, int W, int H, int sW, int sH,
+                              uint32_t* pmap, void* stream);
+
+/* DEVICE: usv_remap_linear_u8 / usv_rectify_pair_u8 through packed maps. */
+usv_status usv_remap_packed_u8(const uint8_t* src, int sW, int sH, int spitch, int cn, const uint32_t* pmap,
+                               int W, int H, uint8_t* dst, int dpitch, void* stream);
+usv_status usv_rectify_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                      int cn, const uint32_t* pmapL, const uint32_t* pmapR, int W, int H,
+                                      uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
+
 /* ---- calibration file: LoadCalibrationData, P/Main.cpp:329-349 ---- */
 
 /* A small dense matrix, row-major doubles (rows = cols = 0: empty, as an unread cv::Mat). */
@@ -419,6 +435,12 @@ usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, in
                                     const uint16_t* map2R, int W, int H, uint8_t* hsvL, uint8_t* hsvR, int hsv_pitch,
                                     uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch, uint8_t* grayL,
                                     uint8_t* grayR, int gray_pitch, void* work, int parity, void* stream);
+/* The same through packed maps (usv_remap_pack_map). */
+usv_status usv_rectify_prep_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                           const uint32_t* pmapL, const uint32_t* pmapR, int W, int H, uint8_t* hsvL,
+                                           uint8_t* hsvR, int hsv_pitch, uint8_t* bgr_outL, uint8_t* bgr_outR,
+                                           int bgr_pitch, uint8_t* grayL, uint8_t* grayR, int gray_pitch, void* work,
+                                           int parity, void* stream);
 
 /* |gray - prev| > thresh -> 255, then erode + dilate with the 5x5 ellipse
  * (gray and prev share pitch). */

@@ -123,6 +123,14 @@ SIGNATURES = {
                                     c_void_p, c_int, c_void_p]),
     "usv_rectify_pair_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "usv_remap_pack_map": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "usv_remap_packed_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
+                                    c_void_p]),
+    "usv_rectify_pair_packed_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "usv_rectify_prep_pair_packed_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                                c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                                c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "usv_bgr2hsv_hist_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "usv_equalize_hsv_bgr_gray_u8": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                              c_void_p, c_int, c_void_p]),

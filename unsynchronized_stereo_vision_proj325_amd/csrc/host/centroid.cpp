@@ -6,9 +6,10 @@
 // VectorCenter_point*.  minAreaRect is OpenCV 3.0 (convexHull by Sklansky's
 // scan on the x-sorted integer points, clockwise, then rotating calipers in
 // float), restated here from its published algorithm: OpenCV is absent from
-// the image, so this row is "parity unpinned" (SURVEY.md §8(c)); its tests are
-// self-consistency checks against an independent restatement plus geometric
-// known answers (tests/test_centroid.py).
+// the image, so this row is "parity unpinned" (SURVEY.md §8(c)); it is
+// bit-exact (every float) against oracle/shape_oracle.c's independent C
+// restatement (tests/test_shape_oracle.py), and tests/test_centroid.py adds
+// geometric known answers and a float64 brute-force minimum rectangle.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>

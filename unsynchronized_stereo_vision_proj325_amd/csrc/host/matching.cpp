@@ -8,8 +8,8 @@
 // so this part is "parity unpinned" against OpenCV itself; it
 // is bit-exact against oracle/shape_oracle.c, an independent C restatement of
 // OpenCV 3.0's contourMoments / HuMoments / matchShapes I1 / contourArea that
-// recomputes every pair as P/Main.cpp:403-426 does (tests/test_shape_oracle.py),
-// plus self-consistency checks (tests/test_matching.py).  Unlike the reference,
+// recomputes every pair as P/Main.cpp:403-426 does (tests/test_shape_oracle.py);
+// tests/test_matching.py adds the method's invariances.  Unlike the reference,
 // which recomputes the moments and four areas for every (i, j) pair
 // (P/Main.cpp:413-414), the invariants are computed once per contour; the
 // per-pair arithmetic on them is unchanged, so the scores are identical.

@@ -283,6 +283,7 @@ struct RectPrepJob {
     RemapJob r;  // r.dst / r.dpitch: the HSV image
     uint32_t* work;
 };
+template <bool PK>
 __global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, RectPrepJob j1, int sW, int sH, int W,
                                                                int H, int blocks_per_job, int vec_map, int vec_src,
                                                                int vec_dst, int parity) {
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, R
     for (int q = blk * 256 + t; q < Q; q += blocks_per_job * 256) {
         const int y = q / nq, x0 = 4 * (q - y * nq), n = min(4, W - x0);
         uint32_t px[12];
-        remap_quad<3>(j.r, sW, sH, W, y, x0, n, vec_map, vec_src, px);
+        remap_quad<3, PK>(j.r, sW, sH, W, y, x0, n, vec_map, vec_src, px);
         Px4 out;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -510,22 +511,27 @@ usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int 
     return usv::st(hipGetLastError());
 }
 
-usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
-                                    const int16_t* map1L, const uint16_t* map2L, const int16_t* map1R,
-                                    const uint16_t* map2R, int W, int H, uint8_t* hsvL, uint8_t* hsvR, int hsv_pitch,
+// usv_rectify_prep_pair_u8 / _packed_u8: jl.r / jr.r carry either map1 + map2 or pmap.
+static usv_status rectify_prep_pair(const usv::RemapJob& jl_r, const usv::RemapJob& jr_r, int sW, int sH, int W, int H,
                                     uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch, uint8_t* grayL,
                                     uint8_t* grayR, int gray_pitch, void* work, int parity, void* stream) {
-    if (!srcL || !srcR || !map1L || !map2L || !map1R || !map2R || !hsvL || !hsvR || !bgr_outL || !bgr_outR ||
-        !grayL || !grayR || !work || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || spitch < 3 * sW ||
-        hsv_pitch < 3 * W || bgr_pitch < 3 * W || gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) ||
-        (long long)W * H > (1LL << 24))
+    const int spitch = jl_r.spitch, hsv_pitch = jl_r.dpitch;
+    uint8_t* hsvL = jl_r.dst;
+    uint8_t* hsvR = jr_r.dst;
+    if (!jl_r.src || !jr_r.src || !hsvL || !hsvR || !bgr_outL || !bgr_outR || !grayL || !grayR || !work || sW <= 0 ||
+        sH <= 0 || W <= 0 || H <= 0 || spitch < 3 * sW || hsv_pitch < 3 * W || bgr_pitch < 3 * W || gray_pitch < W ||
+        !al4(work) || (parity != 0 && parity != 1) || (long long)W * H > (1LL << 24))
         return USV_ERR_INVALID_ARG;
     if ((long long)(sH + 1) * spitch >= (1LL << 32) || spitch >= (1 << 24)) return USV_ERR_UNSUPPORTED;
+    const bool pk = jl_r.pmap != nullptr;
+    if (pk && (sW > usv::kPackMaxSrc || sH > usv::kPackMaxSrc)) return USV_ERR_UNSUPPORTED;
     uint32_t* wL = static_cast<uint32_t*>(work);
     uint32_t* wR = wL + USV_FRAME_PREP_WORK_BYTES / 4;
     auto al = [](const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
-    const int vec_map = (W % 4) == 0 && al(map1L, 16) && al(map1R, 16) && al(map2L, 8) && al(map2R, 8);
-    const int vec_src = al4(srcL) && al4(srcR) && spitch % 4 == 0 && spitch >= 12;
+    const int vec_map = (W % 4) == 0 && (pk ? al(jl_r.pmap, 16) && al(jr_r.pmap, 16)
+                                            : al(jl_r.map1, 16) && al(jr_r.map1, 16) && al(jl_r.map2, 8) &&
+                                                  al(jr_r.map2, 8));
+    const int vec_src = al4(jl_r.src) && al4(jr_r.src) && spitch % 4 == 0 && spitch >= 12;
     const int vec_hsv = al4(hsvL) && al4(hsvR) && hsv_pitch % 4 == 0;
     const int ve = vec_hsv && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) && bgr_pitch % 4 == 0 &&
                    gray_pitch % 4 == 0;
@@ -533,16 +539,42 @@ usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, in
     const long long quads = (long long)((W + 3) / 4) * H;
     const int per_job = (int)std::max<long long>(1, std::min<long long>(1024, (quads + 1023) / 1024));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const usv::RectPrepJob jl{{srcL, spitch, map1L, map2L, hsvL, hsv_pitch}, wL};
-    const usv::RectPrepJob jr{{srcR, spitch, map1R, map2R, hsvR, hsv_pitch}, wR};
-    hipLaunchKernelGGL(usv::rectify_hsv_hist_kernel, dim3(2 * per_job), dim3(256), 0, s, jl, jr, sW, sH, W, H, per_job,
-                       vec_map, vec_src, vec_hsv, parity);
+    const usv::RectPrepJob jl{jl_r, wL};
+    const usv::RectPrepJob jr{jr_r, wR};
+    if (pk)
+        hipLaunchKernelGGL(usv::rectify_hsv_hist_kernel<true>, dim3(2 * per_job), dim3(256), 0, s, jl, jr, sW, sH, W, H,
+                           per_job, vec_map, vec_src, vec_hsv, parity);
+    else
+        hipLaunchKernelGGL(usv::rectify_hsv_hist_kernel<false>, dim3(2 * per_job), dim3(256), 0, s, jl, jr, sW, sH, W,
+                           H, per_job, vec_map, vec_src, vec_hsv, parity);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     const int nb = usv::prep_blocks(W, H);
     hipLaunchKernelGGL(usv::equalize_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s,
                        usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
                        usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
     return usv::st(hipGetLastError());
+}
+
+usv_status usv_rectify_prep_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                    const int16_t* map1L, const uint16_t* map2L, const int16_t* map1R,
+                                    const uint16_t* map2R, int W, int H, uint8_t* hsvL, uint8_t* hsvR, int hsv_pitch,
+                                    uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch, uint8_t* grayL,
+                                    uint8_t* grayR, int gray_pitch, void* work, int parity, void* stream) {
+    if (!map1L || !map2L || !map1R || !map2R) return USV_ERR_INVALID_ARG;
+    return rectify_prep_pair(usv::RemapJob{srcL, spitch, map1L, map2L, hsvL, hsv_pitch},
+                             usv::RemapJob{srcR, spitch, map1R, map2R, hsvR, hsv_pitch}, sW, sH, W, H, bgr_outL,
+                             bgr_outR, bgr_pitch, grayL, grayR, gray_pitch, work, parity, stream);
+}
+
+usv_status usv_rectify_prep_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                           const uint32_t* pmapL, const uint32_t* pmapR, int W, int H, uint8_t* hsvL,
+                                           uint8_t* hsvR, int hsv_pitch, uint8_t* bgr_outL, uint8_t* bgr_outR,
+                                           int bgr_pitch, uint8_t* grayL, uint8_t* grayR, int gray_pitch, void* work,
+                                           int parity, void* stream) {
+    if (!pmapL || !pmapR) return USV_ERR_INVALID_ARG;
+    return rectify_prep_pair(usv::RemapJob{srcL, spitch, nullptr, nullptr, hsvL, hsv_pitch, pmapL},
+                             usv::RemapJob{srcR, spitch, nullptr, nullptr, hsvR, hsv_pitch, pmapR}, sW, sH, W, H,
+                             bgr_outL, bgr_outR, bgr_pitch, grayL, grayR, gray_pitch, work, parity, stream);
 }
 
 usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, int H, int pitch, int thresh,

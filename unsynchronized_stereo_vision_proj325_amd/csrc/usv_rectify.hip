@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
 #define USV_REMAP_XCD 1  // XCD-contiguous block order
 #endif
 constexpr int kRemapBlock = USV_REMAP_BLOCK;
-template <int CN>
+template <int CN, bool PK>
 __global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
                                                     unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
     const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJo
     const int x0 = 4 * (int)(q - (unsigned)y * nq);
     const int n = min(4, W - x0);
     uint32_t out[4 * CN];
-    remap_quad<CN>(j, sW, sH, W, y, x0, n, vec_map, vec_src, out);
+    remap_quad<CN, PK>(j, sW, sH, W, y, x0, n, vec_map, vec_src, out);
     uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
     if (vec_dst && n == 4) {
         if constexpr (CN == 3) {
@@ -112,10 +112,11 @@ bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) %
 
 usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn, int sW, int sH, int W, int H,
                         hipStream_t s) {
+    const bool pk = a.pmap != nullptr;  // both jobs packed or neither (the entry points check)
     bool vec_map = (W % 4) == 0, vec_dst = true, vec_src = true;
     for (int i = 0; i < n_jobs; ++i) {
         const RemapJob& j = i ? b : a;
-        vec_map = vec_map && aligned(j.map1, 16) && aligned(j.map2, 8);
+        vec_map = vec_map && (pk ? aligned(j.pmap, 16) : aligned(j.map1, 16) && aligned(j.map2, 8));
         vec_dst = vec_dst && aligned(j.dst, 4) && (j.dpitch % 4) == 0;
         vec_src = vec_src && aligned(j.src, 4) && (j.spitch % 4) == 0;
     }
@@ -128,20 +129,30 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
     if (a.spitch < 4 * (cn == 1 ? 2 : 3) || b.spitch < 4 * (cn == 1 ? 2 : 3)) vec_src = false;  // rows too short for the aligned reads
     if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
     dim3 grid((unsigned)(per_job * n_jobs)), block(kRemapBlock);
-    if (cn == 1)
-        hipLaunchKernelGGL(remap_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map,
-                           (int)vec_dst, (int)vec_src);
-    else if (cn == 3)
-        hipLaunchKernelGGL(remap_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map,
-                           (int)vec_dst, (int)vec_src);
-    else
-        return USV_ERR_UNSUPPORTED;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, 0, s, a, b, sW, sH, W, H, (unsigned)per_job, (int)vec_map, (int)vec_dst,
+                           (int)vec_src);
+    };
+    if (cn == 1) pk ? go(remap_kernel<1, true>) : go(remap_kernel<1, false>);
+    else if (cn == 3) pk ? go(remap_kernel<3, true>) : go(remap_kernel<3, false>);
+    else return USV_ERR_UNSUPPORTED;
     return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
 }
 
-bool job_ok(const RemapJob& j, int cn, int sW, int W) {
-    return j.src && j.map1 && j.map2 && j.dst && j.spitch >= sW * cn && j.dpitch >= W * cn;
+// map1 / map2 -> the packed word per pixel (usv_remap.hpp pack_map_word); a flat range of pixels.
+__global__ __launch_bounds__(256) void pack_map_kernel(const int16_t* __restrict__ map1,
+                                                       const uint16_t* __restrict__ map2, long long n, int sW, int sH,
+                                                       uint32_t* __restrict__ pmap) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    pmap[i] = pack_map_word(map1[2 * i], map1[2 * i + 1], map2[i], sW, sH);
 }
+
+bool job_ok(const RemapJob& j, int cn, int sW, int W) {
+    return j.src && (j.pmap || (j.map1 && j.map2)) && j.dst && j.spitch >= sW * cn && j.dpitch >= W * cn;
+}
+// the packed map only describes sources of at most kPackMaxSrc columns and rows
+bool packed_ok(int sW, int sH) { return sW <= kPackMaxSrc && sH <= kPackMaxSrc; }
 
 }  // namespace
 }  // namespace usv
@@ -216,6 +227,39 @@ usv_status usv_rectify_pair_u8(const uint8_t* srcL, const uint8_t* srcR, int sW,
     if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
     const usv::RemapJob a{srcL, spitch, map1L, map2L, dstL, dpitch};
     const usv::RemapJob b{srcR, spitch, map1R, map2R, dstR, dpitch};
+    if (!usv::job_ok(a, cn, sW, W) || !usv::job_ok(b, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    return usv::launch_remap(a, b, 2, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+usv_status usv_remap_pack_map(const int16_t* map1, const uint16_t* map2, int W, int H, int sW, int sH, uint32_t* pmap,
+                              void* stream) {
+    if (!map1 || !map2 || !pmap || W <= 0 || H <= 0 || sW <= 0 || sH <= 0) return USV_ERR_INVALID_ARG;
+    if (!usv::packed_ok(sW, sH)) return USV_ERR_UNSUPPORTED;
+    const long long n = (long long)W * H;
+    if ((n + 255) / 256 > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(usv::pack_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), map1, map2, n, sW, sH, pmap);
+    return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
+}
+
+usv_status usv_remap_packed_u8(const uint8_t* src, int sW, int sH, int spitch, int cn, const uint32_t* pmap, int W,
+                               int H, uint8_t* dst, int dpitch, void* stream) {
+    if (!pmap || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    if (!usv::packed_ok(sW, sH)) return USV_ERR_UNSUPPORTED;
+    usv::RemapJob j{src, spitch, nullptr, nullptr, dst, dpitch, pmap};
+    if (!usv::job_ok(j, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    return usv::launch_remap(j, j, 1, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+usv_status usv_rectify_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch, int cn,
+                                      const uint32_t* pmapL, const uint32_t* pmapR, int W, int H, uint8_t* dstL,
+                                      uint8_t* dstR, int dpitch, void* stream) {
+    if (!pmapL || !pmapR || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    if (!usv::packed_ok(sW, sH)) return USV_ERR_UNSUPPORTED;
+    const usv::RemapJob a{srcL, spitch, nullptr, nullptr, dstL, dpitch, pmapL};
+    const usv::RemapJob b{srcR, spitch, nullptr, nullptr, dstR, dpitch, pmapR};
     if (!usv::job_ok(a, cn, sW, W) || !usv::job_ok(b, cn, sW, W)) return USV_ERR_INVALID_ARG;
     return usv::launch_remap(a, b, 2, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
 }

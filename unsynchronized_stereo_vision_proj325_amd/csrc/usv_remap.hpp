@@ -21,7 +21,23 @@ struct RemapJob {
     const uint16_t* map2;
     uint8_t* dst;
     int dpitch;
+    const uint32_t* pmap = nullptr;  // packed map (remap_quad<CN, true>): one word per pixel, see below
 };
+
+// Packed map (usv_remap_pack_map): the CV_16SC2 + CV_16UC1 pair (6 B per pixel) as ONE u32 per pixel,
+// for source images of at most kPackMaxSrc columns and rows:
+//   bits  0..9   the fraction index (map2: (v & 31) * 32 + (u & 31))
+//   bits 10..20  sx + 1,   bits 21..31  sy + 1          (sx, sy = map1's integer source point)
+// A pixel none of whose four taps is inside the source (sx >= sW, sx < -1, sy >= sH or sy < -1) is
+// stored as sx + 1 = sy + 1 = 2047: it decodes to (2046, 2046), which is outside every source the
+// packed form accepts, so it still produces OpenCV's BORDER_CONSTANT 0.  Every other pixel decodes to
+// its exact (sx, sy, fraction): remap results are bit-identical to the 6-byte map's.
+constexpr int kPackMaxSrc = 2046;
+__host__ __device__ __forceinline__ uint32_t pack_map_word(int sx, int sy, int f, int sW, int sH) {
+    const bool any = sx < sW && sx + 1 >= 0 && sy < sH && sy + 1 >= 0;
+    const uint32_t ex = any ? (uint32_t)(sx + 1) : 2047u, ey = any ? (uint32_t)(sy + 1) : 2047u;
+    return ((uint32_t)f & 1023u) | (ex << 10) | (ey << 21);
+}
 
 typedef unsigned short remap_us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t remap_dot2(uint32_t a, uint32_t b, uint32_t c) {
@@ -47,13 +63,27 @@ __device__ __forceinline__ unsigned xcd_block(unsigned lin, unsigned total) {
 //     two taps of a row are one u16 pair and their weights another: two v_dot2_u32_u16 per channel.
 //   * Source offsets are 32-bit (sy * pitch + byte, a 24-bit multiply: pitch < 2^24, checked by the
 //     launchers) from the job's base pointer.
-template <int CN>
+template <int CN, bool PK = false>
 __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, int W, int y, int x0, int n,
                                            int vec_map, int vec_src, uint32_t (&out)[4 * CN]) {
     constexpr int NWD = CN == 1 ? 2 : 3;
     int mx[4], my[4], mf[4];
     const size_t mrow = (size_t)y * W + x0;
-    if (vec_map && n == 4) {
+    if constexpr (PK) {  // one 16-B load for the quad's four packed words
+        uint32_t w4[4];
+        if (vec_map && n == 4) {
+            const uint4 m = *reinterpret_cast<const uint4*>(j.pmap + mrow);
+            w4[0] = m.x; w4[1] = m.y; w4[2] = m.z; w4[3] = m.w;
+        } else {
+            for (int k = 0; k < 4; ++k) w4[k] = j.pmap[mrow + (k < n ? k : 0)];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mf[k] = (int)(w4[k] & 1023u);
+            mx[k] = (int)((w4[k] >> 10) & 2047u) - 1;
+            my[k] = (int)(w4[k] >> 21) - 1;
+        }
+    } else if (vec_map && n == 4) {
 #if USV_REMAP_NT  // the maps are read once per frame: non-temporal loads
         typedef int v4i __attribute__((ext_vector_type(4)));
         typedef unsigned v2u __attribute__((ext_vector_type(2)));

@@ -138,6 +138,15 @@ class FramePrepPair:
             raise ValueError("the two rectifiers must share the output size")
         hl, hr, bl, br, gl, gr = self._outs(src_l, H, W, outs)
         lib = _lib.load()
+        if left.packed_for(src_l) and right.packed_for(src_r):
+            with torch.cuda.device(src_l.device):
+                _lib.check("usv_rectify_prep_pair_packed_u8", lib.usv_rectify_prep_pair_packed_u8(
+                    src_l.data_ptr(), src_r.data_ptr(), sW, sH, src_l.stride(0), left.pmap.data_ptr(),
+                    right.pmap.data_ptr(), W, H, hl.data_ptr(), hr.data_ptr(), hl.stride(0), bl.data_ptr(),
+                    br.data_ptr(), bl.stride(0), gl.data_ptr(), gr.data_ptr(), gl.stride(0), self.work.data_ptr(),
+                    self.parity, _stream(stream)))
+            self.parity ^= 1
+            return (hl, hr), (bl, br), (gl, gr)
         with torch.cuda.device(src_l.device):
             _lib.check("usv_rectify_prep_pair_u8", lib.usv_rectify_prep_pair_u8(
                 src_l.data_ptr(), src_r.data_ptr(), sW, sH, src_l.stride(0), left.map1.data_ptr(),

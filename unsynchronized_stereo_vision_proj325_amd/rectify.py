@@ -5,7 +5,10 @@ The reference rectifies every frame of each camera with
 BORDER_CONSTANT)`` (P/Main.cpp:351-359), rebuilding the map each time because
 the calibration struct is passed by value.  ``Rectifier`` builds the map once on
 the device (usv_rectify_map) and remaps each frame with one HBM-bound gather
-(usv_remap_linear_u8); ``rectify_pair`` does both cameras in one launch.
+(usv_remap_linear_u8); ``rectify_pair`` does both cameras in one launch.  When the
+source is at most 2046 x 2046 the map is also packed into one u32 per pixel
+(usv_remap_pack_map: 4 B instead of 6, bit-identical results) and the frames go
+through the packed form.
 Calibration matrices are the ones ``calibration.load_calibration`` reads.
 """
 from __future__ import annotations
@@ -46,8 +49,14 @@ def _check_u8(t: torch.Tensor, name: str) -> None:
 class Rectifier:
     """One camera's rectification: map built once on `device`, applied per frame."""
 
-    def __init__(self, K, dist, R, P, size: tuple[int, int], device=None, stream=None):
+    PACK_MAX_SRC = 2046  # include/usv.h usv_remap_pack_map
+
+    def __init__(self, K, dist, R, P, size: tuple[int, int], device=None, stream=None,
+                 src_size: tuple[int, int] | None = None, packed: bool = True):
+        """size: output (W, H); src_size: the frames' (W, H) (default: size, as initUndistortRectifyMap's
+        callers use it, P/Main.cpp:352); packed: also build the packed map when the source allows."""
         self.W, self.H = int(size[0]), int(size[1])
+        self.sW, self.sH = (self.W, self.H) if src_size is None else (int(src_size[0]), int(src_size[1]))
         self.params = rectify_params(K, dist, R, P)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.map1 = torch.empty((self.H, self.W, 2), dtype=torch.int16, device=dev)
@@ -57,6 +66,17 @@ class Rectifier:
         with torch.cuda.device(dev):
             _lib.check("usv_rectify_map", lib.usv_rectify_map(p.ctypes.data, self.W, self.H, self.map1.data_ptr(),
                                                               self.map2.data_ptr(), _stream(stream)))
+        self.pmap = None
+        if packed and self.sW <= self.PACK_MAX_SRC and self.sH <= self.PACK_MAX_SRC:
+            self.pmap = torch.empty((self.H, self.W), dtype=torch.int32, device=dev)  # bit pattern of uint32
+            with torch.cuda.device(dev):
+                _lib.check("usv_remap_pack_map", lib.usv_remap_pack_map(
+                    self.map1.data_ptr(), self.map2.data_ptr(), self.W, self.H, self.sW, self.sH,
+                    self.pmap.data_ptr(), _stream(stream)))
+
+    def packed_for(self, src: torch.Tensor) -> bool:
+        """True when frames of src's size go through the packed map."""
+        return self.pmap is not None and (src.shape[1], src.shape[0]) == (self.sW, self.sH)
 
     def maps_numpy(self):
         """(map1 int16 (H, W, 2), map2 uint16 (H, W)) on the host, OpenCV's CV_16SC2 / CV_16UC1 layout."""
@@ -70,6 +90,12 @@ class Rectifier:
                               device=src.device)
         _check_u8(out, "out")
         lib = _lib.load()
+        if self.packed_for(src):
+            with torch.cuda.device(src.device):
+                _lib.check("usv_remap_packed_u8", lib.usv_remap_packed_u8(
+                    src.data_ptr(), src.shape[1], src.shape[0], src.stride(0), cn, self.pmap.data_ptr(), self.W,
+                    self.H, out.data_ptr(), out.stride(0), _stream(stream)))
+            return out
         with torch.cuda.device(src.device):
             _lib.check("usv_remap_linear_u8", lib.usv_remap_linear_u8(
                 src.data_ptr(), src.shape[1], src.shape[0], src.stride(0), cn, self.map1.data_ptr(),
@@ -93,6 +119,13 @@ def rectify_pair(left: Rectifier, right: Rectifier, src_l: torch.Tensor, src_r: 
     if out_l.stride() != out_r.stride():
         raise ValueError("the two outputs must share strides")
     lib = _lib.load()
+    if left.packed_for(src_l) and right.packed_for(src_r):
+        with torch.cuda.device(src_l.device):
+            _lib.check("usv_rectify_pair_packed_u8", lib.usv_rectify_pair_packed_u8(
+                src_l.data_ptr(), src_r.data_ptr(), src_l.shape[1], src_l.shape[0], src_l.stride(0), cn,
+                left.pmap.data_ptr(), right.pmap.data_ptr(), left.W, left.H, out_l.data_ptr(), out_r.data_ptr(),
+                out_l.stride(0), _stream(stream)))
+        return out_l, out_r
     with torch.cuda.device(src_l.device):
         _lib.check("usv_rectify_pair_u8", lib.usv_rectify_pair_u8(
             src_l.data_ptr(), src_r.data_ptr(), src_l.shape[1], src_l.shape[0], src_l.stride(0), cn,
