@@ -216,8 +216,8 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
         "rectify_pair_bgr": (lambda: rectify_pair(rl, rr, src_l, src_r, out_l, out_r), 2 * px * (mb + 3 + 3)),
         # the same through OpenCV's CV_16SC2 + CV_16UC1 map pair (map 4 + 2 B)
         "rectify_pair_bgr_map_pair": (lambda: rectify_pair(ul, ur, src_l, src_r, out_l, out_r), 2 * px * (6 + 3 + 3)),
-        # BGR2HSV+hist (3 in, 3 out) + equalize/HSV2BGR/gray (3 in, 3 + 3 + 1 out), one camera
-        "frame_prep": (lambda: prep(out_l, hsv, bgr2, gray), px * (3 + 3 + 3 + 7)),
+        # V histogram (3 in) + BGR2HSV/equalize/HSV2BGR/gray (3 in, 3 + 3 + 1 out), one camera
+        "frame_prep": (lambda: prep(out_l, hsv, bgr2, gray), px * (3 + 3 + 7)),
         # absdiff + threshold + erode + dilate: gray + prev in, mask out
         "motion_mask": (lambda: ABSDiffSearch(gray, prev, out=mask), px * 3),
     }
@@ -225,16 +225,24 @@ def pipeline_legs(dev, W: int, H: int, steps: int) -> dict:
     pouts = [torch.empty_like(src_l) for _ in range(4)] + [torch.empty((H, W), dtype=torch.uint8, device=dev)
                                                           for _ in range(2)]
     # both cameras' frame prep in two launches (usv_frame_prep_pair_u8)
-    legs["frame_prep_pair"] = (lambda: pair(out_l, out_r, outs=pouts), 2 * px * (3 + 3 + 3 + 7))
+    legs["frame_prep_pair"] = (lambda: pair(out_l, out_r, outs=pouts), 2 * px * (3 + 3 + 7))
     # the whole per-frame stage of the pair in two launches (usv_rectify_prep_pair_u8): rectify + HSV +
     # histogram (4 packed map + 3 src + 3 hsv), then equalize / HSV2BGR / gray (3 + 3 + 3 + 1), per camera
     legs["rectify_prep_pair"] = (lambda: pair.rectify_prep(rl, rr, src_l, src_r, outs=pouts),
                                  2 * px * (mb + 6 + 10))
+    # Size-matched copy roof: a device-to-device copy moving the same bytes (half read, half written),
+    # the rate a stream of this size actually reaches (launch ramp and tail included; 8 TB/s is not
+    # reachable at tens of MB: profiles/probes_r03/stream_probe_r03.txt).
+    cbuf = torch.empty(max(n for _, n in legs.values()), dtype=torch.uint8, device=dev)
     res = {}
     for name, (fn, nbytes) in legs.items():
         us = time_launches(fn, steps, s)
         gbs = nbytes / (us * 1e-6) / 1e9
-        res[name] = {"us": us, "bytes": nbytes, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+        half = nbytes // 2
+        src_c, dst_c = cbuf[:half], cbuf[half:2 * half]
+        copy_us = time_launches(lambda: dst_c.copy_(src_c), steps, s)
+        res[name] = {"us": us, "bytes": nbytes, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
+                     "copy_us_same_bytes": copy_us, "frac_of_copy": copy_us / us}
     return res
 
 

@@ -43,6 +43,8 @@
  *   usv_calibration_rectify_params  XML read without OpenCV)
  *   usv_remap_linear_u8,      remap(INTER_LINEAR, BORDER_CONSTANT, Scalar()),
  *   usv_rectify_pair_u8       P/Main.cpp:353,358 (one launch for both cameras)
+ *   usv_remap_pack_map,       the same remap through a 4-byte-per-pixel form of
+ *   usv_*_packed_u8           the map (built once; results bit-identical)
  *   usv_bgr2hsv_hist_u8,      cvtColor BGR2HSV P/Main.cpp:919 + LightingCorrection
  *   usv_equalize_hsv_bgr_gray_u8  (split/equalizeHist/merge/HSV2BGR,
  *   usv_frame_prep_u8         P/Main.cpp:365-371) + cvtColor BGR2GRAY :921
@@ -414,13 +416,16 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
                                         int hsv_pitch, uint8_t* bgr_out, int bgr_pitch,
                                         uint8_t* gray, int gray_pitch, void* stream);
 
-/* The two calls above: the reference's frame preparation after rectification. */
+/* The reference's frame preparation after rectification: the same outputs as the two calls above, in
+ * two launches that do not materialise the intermediate HSV image (a V = max(B, G, R) histogram pass
+ * that only reads the frame, then BGR2HSV + equalize + HSV2BGR + BGR2GRAY from the frame: 13 B per
+ * pixel instead of 16).  bgr_out may alias bgr. */
 usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv,
                              int hsv_pitch, uint8_t* bgr_out, int bgr_pitch, uint8_t* gray,
                              int gray_pitch, void* work, int parity, void* stream);
 
-/* Both cameras of a pair in two launches (the two calls above, each camera with its own half of
- * `work`, which holds 2 * USV_FRAME_PREP_WORK_BYTES bytes). */
+/* Both cameras of a pair in two launches (usv_frame_prep_u8's two passes, each camera with its own
+ * half of `work`, which holds 2 * USV_FRAME_PREP_WORK_BYTES bytes). */
 usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int W, int H, int pitch, uint8_t* hsvL,
                                   uint8_t* hsvR, int hsv_pitch, uint8_t* bgr_outL, uint8_t* bgr_outR, int bgr_pitch,
                                   uint8_t* grayL, uint8_t* grayR, int gray_pitch, void* work, int parity,

@@ -2,7 +2,7 @@
 """Per-workgroup timeline of the fast kernel from a USV_WGTIME=1 build (GPU box).
 
     scripts/build_variant.sh wgtime -DUSV_WGTIME=1 -DUSV_DEV_ONLY_RAD=5 -DUSV_DEV_ONLY_NW=2
-    USV_LIB_PATH=$PWD/build_variants/wgtime.so python scripts/wgtime.py
+    USV_LIB_PATH=$PWD/build_variants/wgtime.so python scripts/wgtime.py [W H D w]   (default config C)
 
 Prints start/end spread (100 MHz realtime ticks -> us), per-CU workgroup counts
 and the end-time distribution: how much of the launch is tail.
@@ -24,9 +24,10 @@ lib = _lib.load()
 fn = lib.usv_debug_wgtime
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 dev = torch.device("cuda:0")
-L, R, _ = synthetic_pair(1920, 1080, 128, pair_index=0, noise=2)
+W_, H_, D_, w_ = (int(v) for v in sys.argv[1:5]) if len(sys.argv) >= 5 else (1920, 1080, 128, 11)
+L, R, _ = synthetic_pair(W_, H_, D_, pair_index=0, noise=2)
 Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
-m = StereoBlockMatcher(128, 11)
+m = StereoBlockMatcher(D_, w_)
 for _ in range(5):
     m.compute(Lt, Rt, with_distance=True)
 torch.cuda.synchronize()
@@ -86,8 +87,9 @@ for k, v in groups.items():
         spreads.append(v[-1][0] - v[0][0])
         for r, (d, sl, st) in enumerate(v):
             rank_by_slot[sl].append(r)
-print(f"3-wave SIMDs: {len(spreads)}; duration spread (slowest - fastest WG on the SIMD): "
-      f"median {np.median(spreads):.2f} max {np.max(spreads):.2f} us")
+if spreads:
+    print(f"3-wave SIMDs: {len(spreads)}; duration spread (slowest - fastest WG on the SIMD): "
+          f"median {np.median(spreads):.2f} max {np.max(spreads):.2f} us")
 print("mean duration rank (0 fastest .. 2 slowest) by wave slot:",
       {k: round(float(np.mean(v)), 2) for k, v in sorted(rank_by_slot.items())})
 # dispatch model: XCC = lin & 7, generation = (lin >> 3) * NW / (4 * CUs per XCC) -> wave slot

@@ -166,6 +166,65 @@ def test_pair_kernel_pitched_outputs(gpu, dcol, dist_pitch):
     assert (bf[outside] == -1.0).all()
 
 
+@pytest.mark.parametrize("W", [48, 52, 64, 100, 132, 640])
+@pytest.mark.parametrize("D,w", [(64, 7), (34, 5), (18, 9), (32, 5), (62, 9), (40, 7)])
+def test_group_kernel_shapes(gpu, W, D, w):
+    """Grouped paired kernel (usv_sad_group.hip: 16 < D <= 64 even, 5 <= w <= 9): two or four column
+    groups per wave, L staged through LDS with clamped columns (replicate border), the last tile
+    aligned to the right border."""
+    rng = np.random.default_rng(W * 131 + D * 7 + w)
+    H = 45
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    got, dist = gpu_disp(gpu, L, R, D, w, kernel="fast", with_distance=True)
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), (W, D, w, _mismatch(got, ref))
+    lut = distance_lut_cm()
+    assert ((dist == lut[got]) | (np.isinf(dist) & np.isinf(lut[got]))).all()
+
+
+@pytest.mark.parametrize("D,w", [(64, 7), (32, 5)])
+@pytest.mark.parametrize("dcol,dcol_dist,dist_pitch", [(0, 0, 262), (4, 2, 264), (1, 3, 261), (2, 1, 263)])
+def test_group_kernel_pitched_outputs(gpu, D, w, dcol, dcol_dist, dist_pitch):
+    """Group kernel outputs into views of larger buffers: dword / 16-byte stores when the rows allow,
+    byte / double stores otherwise; nothing outside the view is written."""
+    W, H = 224, 61
+    L, R, _ = synthetic_pair(W, H, D, pair_index=3, noise=2)
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+    big_disp = torch.full((H + 2, 260), 77, dtype=torch.uint8, device=gpu)
+    out_disp = big_disp[1:H + 1, dcol:dcol + W]
+    big_dist = torch.full((H + 2, dist_pitch), -1.0, dtype=torch.float64, device=gpu)
+    out_dist = big_dist[1:H + 1, dcol_dist:dcol_dist + W]
+    StereoBlockMatcher(D, w).compute(torch.from_numpy(L).to(gpu), torch.from_numpy(R).to(gpu), with_distance=True,
+                                     out_disp=out_disp, out_dist=out_dist)
+    torch.cuda.synchronize()
+    got = out_disp.cpu().numpy()
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    lut = distance_lut_cm()
+    dd = out_dist.cpu().numpy()
+    assert ((dd == lut[got]) | (np.isinf(dd) & np.isinf(lut[got]))).all()
+    bd = big_disp.cpu().numpy()
+    outside = np.ones(bd.shape, bool)
+    outside[1:H + 1, dcol:dcol + W] = False
+    assert (bd[outside] == 77).all()
+    bf = big_dist.cpu().numpy()
+    outside = np.ones(bf.shape, bool)
+    outside[1:H + 1, dcol_dist:dcol_dist + W] = False
+    assert (bf[outside] == -1.0).all()
+
+
+def test_group_kernel_batch(gpu):
+    """Batched launch through the group kernel (pairs back to back, one launch)."""
+    D, w, W, H = 48, 7, 320, 90
+    pairs = [synthetic_pair(W, H, D, pair_index=i, noise=2) for i in range(3)]
+    Lb = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rb = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    got = StereoBlockMatcher(D, w).compute(Lb, Rb).cpu().numpy()
+    for i, (L, R, _) in enumerate(pairs):
+        ref = oracle_sad(L, R, D, w, "sad", "sliding", threads=THREADS)
+        assert np.array_equal(got[i], ref), (i, _mismatch(got[i], ref))
+
+
 def test_batch_launch(gpu):
     pairs = [synthetic_pair(333, 97, 100, pair_index=i) for i in range(3)]
     L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)

@@ -28,6 +28,11 @@ struct MatchArgs {
 bool fast_path_supported(const MatchArgs& a);
 hipError_t launch_fast(const MatchArgs& a, hipStream_t s);
 
+// Grouped paired-disparity kernel for small disparity ranges (usv_sad_group.hip): SAD, even
+// 16 < D <= 64, 5 <= w <= 9, on shapes fast_path_supported accepts.  hipErrorInvalidValue otherwise.
+bool group_path_supported(const MatchArgs& a);
+hipError_t launch_group(const MatchArgs& a, hipStream_t s);
+
 // Tiled sliding-window path: SAD or SSD, any W / pitch / alignment, odd w <= 31
 // (usv_sad_tiled.hip).  Returns hipErrorInvalidValue outside that range.
 bool tiled_path_supported(const MatchArgs& a);

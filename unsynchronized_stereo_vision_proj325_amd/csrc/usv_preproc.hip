@@ -8,6 +8,8 @@
 //                        LUT[V] written back into the HSV image (merge through
 //                        the shared Mat, P/Main.cpp:369), HSV2BGR (P/Main.cpp:370)
 //                        and BGR2GRAY (P/Main.cpp:921) in one pass
+//   v_hist_kernel +      usv_frame_prep_u8 / _pair_u8: the histogram of V = max(B,G,R) (reads only),
+//   equalize_kernel<1>   then the pass above recomputing BGR2HSV from the frame (no HSV intermediate)
 //   mask_kernel<MODE>    absdiff > 40 (ABSDiffSearch, P/Main.cpp:304-308) or two
 //                        inRange + saturating add (ColourSearch, P/Main.cpp:322-324),
 //                        then erode + dilate with the 5x5 ellipse
@@ -181,6 +183,43 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
     }
 }
 
+// Histogram of V = max(B, G, R) only (RGB2HSV_b's v; P/Main.cpp:368 equalizes that channel): the
+// first pass of usv_frame_prep_u8 / _pair_u8, which reads the frame and writes nothing but the
+// workspace histograms (per-wave LDS copies, one global add per occupied bin and block, the other
+// parity cleared by block 0, as hsv_hist_kernel).
+__global__ __launch_bounds__(kPT) void v_hist_kernel(HistJob j0, HistJob j1, int W, int H, int parity,
+                                                     int blocks_per_job, int vec) {
+    constexpr int NWV = kPT / 64;
+    const int job = (int)blockIdx.x >= blocks_per_job ? 1 : 0;
+    const int blk = (int)blockIdx.x - job * blocks_per_job;
+    const HistJob& j = job ? j1 : j0;
+    uint32_t* __restrict__ work = j.work;
+    __shared__ uint32_t lh[NWV][256];
+    const int t = threadIdx.x, wv = t >> 6;
+    const bool vec4 = vec && (W & 3) == 0;
+    for_each_quad(
+        W, H, vec4, blk, blocks_per_job,
+        [&](int y, int x, int n, bool v) { return load_px4(j.bgr + (size_t)y * j.pitch + 3 * x, v, n); },
+        [&] {
+            for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
+            if (blk == 0 && t < 256)
+                for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
+            __syncthreads();
+        },
+        [&](int, int, int n, bool, const Px4& in) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < n) atomicAdd(&lh[wv][max(max(in.c[3 * k], in.c[3 * k + 1]), in.c[3 * k + 2])], 1u);
+        });
+    __syncthreads();
+    if (t < 256) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) sum += lh[w][t];
+        if (sum) atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blk % kHistCopies) + t], sum);
+    }
+}
+
 // One camera's equalize pass: the histogram it reads and the images it rewrites.
 struct EqJob {
     const uint32_t* work;
@@ -190,6 +229,8 @@ struct EqJob {
     int bgr_pitch;
     uint8_t* gray;
     int gray_pitch;
+    const uint8_t* src = nullptr;  // FROM_BGR: the BGR frame HSV is recomputed from (hsv is output only)
+    int src_pitch = 0;
 };
 
 // V' = LUT[V] written back into hsv, HSV2BGR, BGR2GRAY; kU quads per thread.  Blocks
@@ -197,8 +238,14 @@ struct EqJob {
 // equalizeHist LUT comes from the job's complete histogram, built by the block's first 256 threads
 // while the first sweep's pixel loads are in flight: an inclusive scan within each wave by shuffles
 // plus the four wave totals, then OpenCV's float scale and cvRound.
+// FROM_BGR (usv_frame_prep_u8 / _pair_u8): the pass reads the BGR frame instead of an HSV image and
+// recomputes BGR2HSV (the same integer tables as hsv_hist_kernel), so the first pass only has to
+// histogram V = max(B, G, R) (v_hist_kernel) and no HSV intermediate crosses HBM: 13 B per pixel
+// instead of 16, outputs bit-identical.
+template <bool FROM_BGR>
 __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int parity, int W, int H,
                                                        int blocks_per_job, int vec) {
+    __shared__ int sdiv[FROM_BGR ? 256 : 1], hdiv[FROM_BGR ? 256 : 1];
     __shared__ int scan[256];
     __shared__ int first;
     __shared__ uint8_t lut[256];
@@ -207,6 +254,7 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
     const EqJob& j = job ? j1 : j0;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     auto build_lut = [&] {
+        if constexpr (FROM_BGR) hsv_tables(sdiv, hdiv);  // (read after the barriers below)
         int x = 0;
         if (t < 256) {
             int hv = 0;
@@ -249,11 +297,24 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
         W, H, vec4, (int)blockIdx.x - job * blocks_per_job, blocks_per_job,
-        [&](int y, int x, int n, bool v) { return load_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, v, n); },
+        [&](int y, int x, int n, bool v) {
+            if constexpr (FROM_BGR) return load_px4(j.src + (size_t)y * j.src_pitch + 3 * x, v, n);
+            else return load_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, v, n);
+        },
         build_lut,
         [&](int y, int x, int n, bool v, Px4 in) {
             Px4 o;
             uint32_t g4 = 0;
+            if constexpr (FROM_BGR) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    int h, sat, val;
+                    bgr2hsv_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], sdiv, hdiv, h, sat, val);
+                    in.c[3 * k] = h;
+                    in.c[3 * k + 1] = sat;
+                    in.c[3 * k + 2] = val;
+                }
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
@@ -473,7 +534,7 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
                     gray_pitch % 4 == 0;
     const usv::EqJob j{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch};
     const int nb = usv::prep_blocks(W, H);
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j,
+    hipLaunchKernelGGL(usv::equalize_kernel<false>, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j,
                        parity, W, H, nb, vec);
     return usv::st(hipGetLastError());
 }
@@ -481,10 +542,23 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
 usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_t* hsv, int hsv_pitch,
                              uint8_t* bgr_out, int bgr_pitch, uint8_t* gray, int gray_pitch, void* work,
                              int parity, void* stream) {
-    usv_status r = usv_bgr2hsv_hist_u8(bgr, W, H, pitch, hsv, hsv_pitch, work, parity, stream);
-    if (r != USV_OK) return r;
-    return usv_equalize_hsv_bgr_gray_u8(work, parity, hsv, W, H, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
-                                        stream);
+    // V histogram (reads only), then BGR2HSV + equalize + HSV2BGR + gray from the BGR frame
+    if (!bgr || !hsv || !bgr_out || !gray || !work || W <= 0 || H <= 0 || pitch < 3 * W || hsv_pitch < 3 * W ||
+        bgr_pitch < 3 * W || gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) ||
+        (long long)W * H > (1LL << 24))
+        return USV_ERR_INVALID_ARG;
+    const int vh = al4(bgr) && pitch % 4 == 0;
+    const int ve = vh && al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
+                   gray_pitch % 4 == 0;
+    const usv::HistJob hj{bgr, pitch, nullptr, 0, static_cast<uint32_t*>(work)};
+    const int nb = usv::prep_blocks(W, H);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(nb), dim3(usv::kPT), 0, s, hj, hj, W, H, parity, nb, vh);
+    if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
+    const usv::EqJob ej{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
+                        bgr, pitch};
+    hipLaunchKernelGGL(usv::equalize_kernel<true>, dim3(nb), dim3(usv::kPT), 0, s, ej, ej, parity, W, H, nb, ve);
+    return usv::st(hipGetLastError());
 }
 
 usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int W, int H, int pitch, uint8_t* hsvL,
@@ -497,17 +571,19 @@ usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int 
         return USV_ERR_INVALID_ARG;
     uint32_t* wL = static_cast<uint32_t*>(work);
     uint32_t* wR = wL + USV_FRAME_PREP_WORK_BYTES / 4;
-    const int vh = al4(bgrL) && al4(bgrR) && al4(hsvL) && al4(hsvR) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
-    const int ve = al4(hsvL) && al4(hsvR) && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) &&
+    // V histograms (reads only), then BGR2HSV + equalize + HSV2BGR + gray from the BGR frames
+    const int vh = al4(bgrL) && al4(bgrR) && pitch % 4 == 0;
+    const int ve = vh && al4(hsvL) && al4(hsvR) && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) &&
                    hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 && gray_pitch % 4 == 0;
     const int nb = usv::prep_blocks(W, H);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, hsvL, hsv_pitch, wL},
-                       usv::HistJob{bgrR, pitch, hsvR, hsv_pitch, wR}, W, H, parity, nb, vh);
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, nullptr, 0, wL},
+                       usv::HistJob{bgrR, pitch, nullptr, 0, wR}, W, H, parity, nb, vh);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s,
-                       usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
-                       usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
+    hipLaunchKernelGGL(usv::equalize_kernel<true>, dim3(2 * nb), dim3(usv::kPT), 0, s,
+                       usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch, bgrL, pitch},
+                       usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch, bgrR, pitch}, parity, W, H,
+                       nb, ve);
     return usv::st(hipGetLastError());
 }
 
@@ -549,7 +625,7 @@ static usv_status rectify_prep_pair(const usv::RemapJob& jl_r, const usv::RemapJ
                            H, per_job, vec_map, vec_src, vec_hsv, parity);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     const int nb = usv::prep_blocks(W, H);
-    hipLaunchKernelGGL(usv::equalize_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s,
+    hipLaunchKernelGGL(usv::equalize_kernel<false>, dim3(2 * nb), dim3(usv::kPT), 0, s,
                        usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
                        usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
     return usv::st(hipGetLastError());

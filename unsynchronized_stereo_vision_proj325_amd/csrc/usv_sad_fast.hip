@@ -32,6 +32,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "usv_band.hpp"
 #include "usv_kernels.hpp"
 
 namespace usv {
@@ -124,18 +125,23 @@ struct Cfg {
 //              may overlap its neighbour; both write identical values):
 //              load up to column W-1, the last r positions replicate it.
 enum : int { kInterior = 0, kLeft = 1, kRight = 2 };
+//   (an edge segment shorter than 4 dwords -- K = 8 with r <= 4 -- is loaded as 4: the left one reads
+//   on past its last byte, the right one starts PAD dwords earlier, so neither leaves the row)
 template <int RAD, int EDGE, int KK = kK>
 struct LSeg {
     static constexpr int K = KK, NPOS = K + 2 * RAD;
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - r) mod 4 for x0 % 4 == 0
-    static constexpr int NLD = EDGE == kInterior ? (LOFF + NPOS + 3) / 4
-                             : EDGE == kLeft     ? (K + RAD + 3) / 4
-                                                 : (LOFF + K + RAD) / 4;
-    __device__ static constexpr int base(int x0) { return EDGE == kLeft ? 0 : x0 - RAD - LOFF; }
+    static constexpr int NLD0 = EDGE == kInterior ? (LOFF + NPOS + 3) / 4
+                              : EDGE == kLeft     ? (K + RAD + 3) / 4
+                                                  : (LOFF + K + RAD) / 4;
+    static constexpr int PAD = NLD0 < 4 ? 4 - NLD0 : 0;
+    static constexpr int NLD = NLD0 + PAD;
+    static constexpr int SHIFT = EDGE == kRight ? 4 * PAD : 0;  // bytes the right segment starts early
+    __device__ static constexpr int base(int x0) { return EDGE == kLeft ? 0 : x0 - RAD - LOFF - SHIFT; }
     __device__ static constexpr int byte(int j) {
         return EDGE == kInterior ? LOFF + j
              : EDGE == kLeft     ? (j < RAD ? 0 : j - RAD)
-                                 : (LOFF + j < LOFF + K + RAD - 1 ? LOFF + j : LOFF + K + RAD - 1);
+                                 : SHIFT + (LOFF + j < LOFF + K + RAD - 1 ? LOFF + j : LOFF + K + RAD - 1);
     }
     static_assert(EDGE != kRight || (LOFF + K + RAD) % 4 == 0, "right segment ends on a dword");
     static_assert(NLD >= 4 && NLD <= 8 && (NLD != 7 || K == 12), "scalar segment is 4, 5, 6 or 8 dwords (7: K = 12, loaded as 8)");
@@ -910,18 +916,10 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
     const unsigned pair = past ? 0u : tile / per_pair;
     const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
     const unsigned long_run = base + 1u, split = rem * long_run;
-    auto gen_weight = [&](unsigned sb) -> unsigned {
-        const unsigned t = pair * per_pair + sb * nxt + col_xt;  // tile carrying band sb of this column
-        const unsigned j = t < split ? t % long_run : (t - split) % base;
-        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
-        return (P.weights >> (8 * g)) & 0xFFu;
-    };
-    unsigned pre = 0, tot = 0;
-    for (unsigned sb = 0; sb < m_col; ++sb) {
-        const unsigned wgt = gen_weight(sb);
-        pre += sb < s ? wgt : 0u;
-        tot += wgt;
-    }
+    // weight sums of the column's bands (usv_band.hpp: one band per lane, three wave sums)
+    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
+                                  (unsigned)P.gen_g, P.weights);
+    const unsigned pre = bs.pre, tot = bs.tot;
     const unsigned col = pair * nxt + col_xt;
     const int xt = (int)(col % (unsigned)P.n_xt);
     const int band = (int)s;
@@ -933,7 +931,7 @@ __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(co
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
     const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     L += b * a.pair_stride;
     R += b * a.pair_stride;
     disp += b * a.disp_stride;
@@ -1097,7 +1095,7 @@ struct PCfg {
     static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
     static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
-    static_assert(RAD >= 5 && RAD <= 7, "paired kernel: 11 <= w <= 15");
+    static_assert(RAD >= 2 && RAD <= 7, "paired kernel: 5 <= w <= 15");
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
 };
@@ -2001,25 +1999,16 @@ __global__ __launch_bounds__(64, USV_P16_OCC) void sad_pair16_kernel(const uint8
     const unsigned pair = past ? 0u : tile / per_pair;
     const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
     const unsigned long_run = base + 1u, split = rem * long_run;
-    auto gen_weight = [&](unsigned sb) -> unsigned {
-        const unsigned t = pair * per_pair + sb * nxt + col_xt;
-        const unsigned j = t < split ? t % long_run : (t - split) % base;
-        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
-        return (P.weights >> (8 * g)) & 0xFFu;
-    };
-    unsigned pre = 0, tot = 0;
-    for (unsigned sb = 0; sb < m_col; ++sb) {
-        const unsigned wgt = gen_weight(sb);
-        pre += sb < s ? wgt : 0u;
-        tot += wgt;
-    }
+    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
+                                  (unsigned)P.gen_g, P.weights);
+    const unsigned pre = bs.pre, tot = bs.tot;
     const int xt = (int)col_xt;
     const int n_xt = P.n_xt;
     int x0 = xt * C::K;
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
     const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
@@ -2066,25 +2055,16 @@ __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(co
     const unsigned pair = past ? 0u : tile / per_pair;
     const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
     const unsigned long_run = base + 1u, split = rem * long_run;
-    auto gen_weight = [&](unsigned sb) -> unsigned {
-        const unsigned t = pair * per_pair + sb * nxt + col_xt;
-        const unsigned j = t < split ? t % long_run : (t - split) % base;
-        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
-        return (P.weights >> (8 * g)) & 0xFFu;
-    };
-    unsigned pre = 0, tot = 0;
-    for (unsigned sb = 0; sb < m_col; ++sb) {
-        const unsigned wgt = gen_weight(sb);
-        pre += sb < s ? wgt : 0u;
-        tot += wgt;
-    }
+    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
+                                  (unsigned)P.gen_g, P.weights);
+    const unsigned pre = bs.pre, tot = bs.tot;
     const int xt = (int)col_xt;
     const int n_xt = P.n_xt;
     int x0 = xt * C::K;
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
     const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
@@ -2542,25 +2522,16 @@ __device__ __forceinline__ TileWork tile_work(const BandPlan& P, const MatchArgs
     const unsigned pair = past ? 0u : tile / per_pair;
     const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
     const unsigned long_run = base + 1u, split = rem * long_run;
-    auto gen_weight = [&](unsigned sb) -> unsigned {
-        const unsigned t = pair * per_pair + sb * nxt + col_xt;
-        const unsigned j = t < split ? t % long_run : (t - split) % base;
-        const unsigned g = min(j / (unsigned)P.gen_g, 3u);
-        return (P.weights >> (8 * g)) & 0xFFu;
-    };
-    unsigned pre = 0, tot = 0;
-    for (unsigned sb = 0; sb < m_col; ++sb) {
-        const unsigned wgt = gen_weight(sb);
-        pre += sb < s ? wgt : 0u;
-        tot += wgt;
-    }
+    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
+                                  (unsigned)P.gen_g, P.weights);
+    const unsigned pre = bs.pre, tot = bs.tot;
     TileWork tw;
     tw.xt = (int)col_xt;
     tw.x0 = tw.xt * K;
     if (tw.xt == P.n_xt - 1) tw.x0 = a.W - K;
     else if (tw.xt == P.n_xt - 2) tw.x0 = min(tw.x0, a.W - 2 * K);
     tw.y_begin = (int)((unsigned long long)a.H * pre / tot);
-    tw.y_end = (int)((unsigned long long)a.H * (pre + gen_weight(s)) / tot);
+    tw.y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     tw.pair = pair;
     return tw;
 }
@@ -2651,7 +2622,11 @@ hipError_t launch_ssd_r(const MatchArgs& a, hipStream_t s) {
 #ifndef USV_PAIR
 #define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
 #endif
+#ifndef USV_PAIR_SMALL
+#define USV_PAIR_SMALL 0  // experiment: the paired kernel also for even 32 < D <= 64 and 5 <= w <= 9
+#endif
 bool pair_path_supported(const MatchArgs& a) {
+    if (USV_PAIR_SMALL && a.D > 32 && a.D <= 64 && (a.D % 2) == 0 && a.w >= 5 && a.w <= 9) return true;
     return USV_PAIR && a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15;
 }
 template <int RAD>
@@ -2712,9 +2687,15 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
     if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
     return a.w == 11 ? launch_pair_r<5>(a, s) : a.w == 15 ? launch_pair_r<7>(a, s) : hipErrorInvalidValue;
 #else
+    if (group_path_supported(a)) return launch_group(a, s);  // usv_sad_group.hip: D <= 64, w <= 9
     if (pair_path_supported(a)) {
         if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
         switch ((a.w - 1) / 2) {
+#if USV_PAIR_SMALL
+            case 2: return launch_pair_r<2>(a, s);
+            case 3: return launch_pair_r<3>(a, s);
+            case 4: return launch_pair_r<4>(a, s);
+#endif
             case 5: return launch_pair_r<5>(a, s);
             case 6: return launch_pair_r<6>(a, s);
             case 7: return launch_pair_r<7>(a, s);
