@@ -76,10 +76,11 @@ def _sregs(tok):
 def fast_kernels(tmp_path_factory):
     funcs = _disassembly(tmp_path_factory.mktemp("isa"))
     fast = {k: v for k, v in funcs.items()
-            if "sad_fast_kernel" in k or "sad_pair_kernel" in k or "ssd_fast_kernel" in k}
+            if "sad_fast_kernel" in k or "sad_pair_kernel" in k or "ssd_fast_kernel" in k or "sad_group_kernel" in k}
     assert sum("sad_fast_kernel" in k for k in fast) == 21, sorted(fast)  # r = 1..7 x NW = 1, 2, 4
     assert sum("sad_pair_kernel" in k for k in fast) == 6, sorted(fast)   # r = 5..7 x NW = 1, 2
     assert sum("ssd_fast_kernel" in k for k in fast) == 9, sorted(fast)   # r = 5..7 x NW = 1, 2, 4
+    assert sum("sad_group_kernel" in k for k in fast) == 6, sorted(fast)  # r = 2..4 x G = 2, 4
     return fast
 
 

@@ -377,6 +377,16 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// The 2 KB distance table into LDS by two 16-byte-per-lane LDS-DMAs, issued ahead of a band loop's row
+// prologue: vector-memory ops retire in order, so the first row's counted DMA wait also retires them, and
+// nothing waits on the table's own round trip (a register load + ds_write + barrier waited vmcnt(0)).
+// Every wave of a workgroup stages the whole table (identical bytes): no barrier before its first use.
+__device__ __forceinline__ void lut_dma(const double* lut, uint32_t* lds, int lane) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2\n\t"
+                 "global_load_lds_dwordx4 %0, %2 offset:1024"
+                 :: "v"((uint32_t)lane * 16u), "s"(lds_addr(lds)), "s"(lut) : "memory", "m0");
+}
+
 // Scalar-load an exact number of dwords (5, 6 or 8: never past the row) into SGPRs.
 // Two-instruction forms use early-clobber outputs: the first load's
 // destination must not overlap the base the second one reads.
@@ -1596,6 +1606,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
     uint32_t ring[WIN][K];
+    static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
+    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
     [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
     using WarmT = std::integral_constant<bool, true>;
@@ -1943,6 +1955,8 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
     uint32_t ring[WIN][K];
+    static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
+    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
     [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
     using WarmT = std::integral_constant<bool, true>;
@@ -2012,12 +2026,7 @@ __global__ __launch_bounds__(64, USV_P16_OCC) void sad_pair16_kernel(const uint8
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
-    if (dist) {
-        dist += (size_t)pair * a.dist_stride;
-        double* lut_s = reinterpret_cast<double*>(smem + C::LUT_OFF);
-        for (int i = threadIdx.x; i < 256; i += 64) lut_s[i] = a.lut[i];
-    }
-    __syncthreads();
+    if (dist) dist += (size_t)pair * a.dist_stride;  // (the table is staged inside the band loop)
     if (y_end <= y_begin) return;
     if (xt == 0)
         pair16_band_loop<RAD, KK, kLeft>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
@@ -2068,12 +2077,7 @@ __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(co
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
-    if (dist) {
-        dist += (size_t)pair * a.dist_stride;
-        double* lut_s = reinterpret_cast<double*>(smem + C::LUT_OFF);
-        for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
-    }
-    __syncthreads();
+    if (dist) dist += (size_t)pair * a.dist_stride;  // (the table is staged inside the band loop)
     if (y_end <= y_begin) return;
     if (xt == 0)
         pair_band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
@@ -2469,6 +2473,8 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
     uint32_t ring[WIN][K];
+    static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
+    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
     [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
     using WarmT = std::integral_constant<bool, true>;
@@ -2553,12 +2559,7 @@ __global__ __launch_bounds__(NW * 64, ssd_occ(RAD)) void ssd_fast_kernel(const u
     L += (size_t)tw.pair * a.pair_stride;
     R += (size_t)tw.pair * a.pair_stride;
     disp += (size_t)tw.pair * a.disp_stride;
-    if (dist) {
-        dist += (size_t)tw.pair * a.dist_stride;
-        double* lut_s = reinterpret_cast<double*>(smem + C::LUT_OFF);
-        for (int i = threadIdx.x; i < 256; i += NW * 64) lut_s[i] = a.lut[i];
-    }
-    __syncthreads();
+    if (dist) dist += (size_t)tw.pair * a.dist_stride;  // (the table is staged inside the band loop)
     if (tw.y_end <= tw.y_begin) return;
     if (tw.xt == 0)
         ssd_band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, tw.x0, tw.y_begin, tw.y_end);

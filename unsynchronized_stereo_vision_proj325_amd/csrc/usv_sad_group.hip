@@ -97,7 +97,7 @@ struct GCfg {
     static constexpr int RBUF_OFF = 0;
     static constexpr int TB_OFF = RBUF_OFF + NB * SLOT;
     static constexpr int COMB_OFF = TB_OFF + K * 64;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * KW;
+    static constexpr int LUT_OFF = (COMB_OFF + 2 * KRB * KW + 3) / 4 * 4;  // 16-byte aligned (LDS-DMA x4)
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
     static_assert(G == 2 || G == 4, "two or four column groups");
     static_assert(RAD >= 1 && RAD <= 7, "packed-u16 costs: w <= 15");
@@ -170,6 +170,12 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
             issue_dma(t + PD, (uint32_t)min(max(rr, 0), last_off));
             raw = rr + a.pitch;
         }
+        // the ring row leaving the window is subtracted first: its registers are then free for this row's
+        // H (no copies at the ring write below)
+        if constexpr (!WARM) {
+#pragma unroll
+            for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        }
         int boff = (t & (NB - 1)) * C::SLOT;
         asm volatile("" : "+s"(boff));
         const uint32_t* slot = smem + C::RBUF_OFF + boff;
@@ -197,8 +203,7 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
 #pragma unroll
         for (int x = 0; x < K; ++x) {
             const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
-            if constexpr (WARM) S[x] = S[x] + h;
-            else S[x] = (S[x] - ring[I][x]) + h;
+            S[x] = S[x] + h;  // (S - ring is a (w - 1)-row sum: no half leaves [0, 65535])
             ring[I][x] = h;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -275,6 +280,13 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
     uint32_t ring[WIN][K];
+    // The 2 KB distance table goes to LDS by two 16-byte-per-lane LDS-DMAs issued ahead of the row
+    // prologue: vector-memory ops retire in order, so the first row's counted wait also retires them and
+    // nothing waits for the table's round trip on its own (a register load + ds_write would wait vmcnt(0)).
+    if (dist)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2\n\t"
+                     "global_load_lds_dwordx4 %0, %2 offset:1024"
+                     :: "v"((uint32_t)lane * 16u), "s"(g_lds_addr(smem + C::LUT_OFF)), "s"(a.lut) : "memory", "m0");
     // prologue: PD rows in flight
 #pragma unroll
     for (int t = 0; t < PD; ++t) issue_dma(t, row_off(t));
@@ -342,12 +354,7 @@ __global__ __launch_bounds__(64, USV_GROUP_OCC) void sad_group_kernel(const uint
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
-    if (dist) {
-        dist += (size_t)pair * a.dist_stride;
-        double* lut_s = reinterpret_cast<double*>(smem + C::LUT_OFF);
-        for (int i = threadIdx.x; i < 256; i += 64) lut_s[i] = a.lut[i];
-    }
-    __syncthreads();
+    if (dist) dist += (size_t)pair * a.dist_stride;  // (its table is staged inside the band loop)
     if (y_end <= y_begin) return;
     group_band_loop<RAD, G>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
 }
@@ -374,7 +381,10 @@ int group_cu_count() {
 }
 
 #ifndef USV_GROUP_MIN_BAND_WINS
-#define USV_GROUP_MIN_BAND_WINS 3  // shortest band, in windows (the ring warm-up costs w rows per band)
+#define USV_GROUP_MIN_BAND_WINS 1  // shortest band, in windows (the ring warm-up costs w rows per band)
+#endif
+#ifndef USV_GROUP_MIN_BAND_ROWS
+#define USV_GROUP_MIN_BAND_ROWS 0  // experiment: shortest band in rows (0: USV_GROUP_MIN_BAND_WINS windows)
 #endif
 #ifndef USV_GROUP_WEIGHTS
 #define USV_GROUP_WEIGHTS 0x01010101u  // band heights by dispatch generation (uniform until fitted)
@@ -389,11 +399,12 @@ hipError_t launch_group_rg(const MatchArgs& a, hipStream_t s) {
     const long NC = (long)P.n_xt * a.batch;
     long m = slots / NC;
     if (m < 1) m = 1;
-    const long m_max = a.H / (USV_GROUP_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_GROUP_MIN_BAND_WINS * WIN) : 1;
+    const long min_rows = USV_GROUP_MIN_BAND_ROWS > 0 ? USV_GROUP_MIN_BAND_ROWS : USV_GROUP_MIN_BAND_WINS * WIN;
+    const long m_max = a.H / min_rows > 0 ? a.H / min_rows : 1;
     if (m > m_max) m = m_max;
     P.m = (int)m;
     const long ex = slots - NC * m;
-    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt && a.H / (m + 1) >= USV_GROUP_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt && a.H / (m + 1) >= min_rows) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     P.gen_g = (int)(4L * (group_cu_count() / 8));
