@@ -98,6 +98,8 @@ def fast_kernel_name(W: int, D: int, w: int, pitch: int) -> str:
     """Which kernel the AUTO dispatch takes for this shape (csrc/usv_sad_fast.hip
     fast_path_supported / pair_path_supported / launch_fast), for labelling the roofline entry."""
     if 3 <= w <= 15 and w % 2 == 1 and 1 <= D <= 256 and W % 4 == 0 and W >= 48 and pitch % 4 == 0:
+        if D % 2 == 0 and 16 < D <= 64 and 5 <= w <= 9:  # csrc/usv_sad_group.hip group_path_supported
+            return f"sad_group_kernel<{(w - 1) // 2}, {2 if D > 32 else 4}>"
         if D > 64 and D % 2 == 0 and w >= 11:
             return f"sad_pair_kernel<{(w - 1) // 2}, {1 if D <= 128 else 2}>"
         nw = 1 if D <= 64 else (2 if D <= 128 else 4)
