@@ -67,31 +67,26 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
     }
 }
 
-// One quad (4 output pixels) per thread over a flat, XCD-contiguous range of quads per camera;
-// remap_quad (usv_remap.hpp) computes it, the result leaves as one 4-B (gray) or one 12-B (BGR)
-// store.  (Two or four quads per thread with every load issued first ran slower: 18.1 / 24.6 us
-// vs 15.1 us for the 1080p BGR pair on one box.)
+// Quads (4 output pixels) over a flat, XCD-contiguous range per camera; remap_quad (usv_remap.hpp)
+// computes one, the result leaves as one 4-B (gray) or one 12-B (BGR) store.  A thread takes kRemapQPT
+// quads, a grid-stride apart, and has the NEXT quad's map words in flight while it gathers and blends
+// the current one: with one quad per thread every wave was a dependent map-load -> source-load ->
+// store chain, and the launch ran at two such chains' latency (without any source reads at all it
+// still took 11.4 of its 13.7 us; profiles/probes_r03/ab_remap_gather_r03.txt).
 #ifndef USV_REMAP_BLOCK
 #define USV_REMAP_BLOCK 256  // threads per block
 #endif
 #ifndef USV_REMAP_XCD
 #define USV_REMAP_XCD 1  // XCD-contiguous block order
 #endif
+#ifndef USV_REMAP_QPT
+#define USV_REMAP_QPT 4  // quads per thread (map prefetched one quad ahead)
+#endif
 constexpr int kRemapBlock = USV_REMAP_BLOCK;
-template <int CN, bool PK>
-__global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
-                                                    unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
-    const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const unsigned job = lb >= blocks_per_job ? 1u : 0u;
-    const RemapJob& j = job ? j1 : j0;
-    const unsigned nq = (unsigned)(W + 3) >> 2;
-    const unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
-    if (q >= nq * (unsigned)H) return;
-    const int y = (int)(q / nq);
-    const int x0 = 4 * (int)(q - (unsigned)y * nq);
-    const int n = min(4, W - x0);
-    uint32_t out[4 * CN];
-    remap_quad<CN, PK>(j, sW, sH, W, y, x0, n, vec_map, vec_src, out);
+constexpr int kRemapQPT = USV_REMAP_QPT;
+template <int CN>
+__device__ __forceinline__ void remap_store(const RemapJob& j, int y, int x0, int n, int vec_dst,
+                                            const uint32_t (&out)[4 * CN]) {
     uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
     if (vec_dst && n == 4) {
         if constexpr (CN == 3) {
@@ -105,6 +100,40 @@ __global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJo
         }
     } else {
         for (int b = 0; b < n * CN; ++b) d[b] = (uint8_t)out[b];
+    }
+}
+template <int CN, bool PK>
+__global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
+                                                    unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
+    const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const unsigned job = lb >= blocks_per_job ? 1u : 0u;
+    const RemapJob& j = job ? j1 : j0;
+    const unsigned nq = (unsigned)(W + 3) >> 2, total = nq * (unsigned)H;
+    const unsigned stride = blocks_per_job * (unsigned)kRemapBlock;
+    unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
+    if (q >= total) return;
+    auto where = [&](unsigned qq, int& y, int& x0, int& n) {
+        y = (int)(qq / nq);
+        x0 = 4 * (int)(qq - (unsigned)y * nq);
+        n = min(4, W - x0);
+    };
+    int y, x0, n;
+    where(q, y, x0, n);
+    RemapMapRaw next = remap_map_load<PK>(j, W, y, x0, n, vec_map);
+    for (;;) {
+        const RemapMapRaw cur = next;
+        const int cy = y, cx0 = x0, cn = n;
+        const unsigned qn = q + stride;
+        const bool more = qn < total;
+        if (more) {  // the next quad's map is in flight during this quad's gathers
+            where(qn, y, x0, n);
+            next = remap_map_load<PK>(j, W, y, x0, n, vec_map);
+        }
+        uint32_t out[4 * CN];
+        remap_quad_from<CN, PK>(j, cur, sW, sH, vec_src, out);
+        remap_store<CN>(j, cy, cx0, cn, vec_dst, out);
+        if (!more) break;
+        q = qn;
     }
 }
 
@@ -125,7 +154,7 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
         a.spitch >= (1 << 24) || b.spitch >= (1 << 24))
         return USV_ERR_UNSUPPORTED;
     const long long quads = (long long)((W + 3) / 4) * H;
-    const long long per_job = (quads + kRemapBlock - 1) / kRemapBlock;
+    const long long per_job = (quads + (long long)kRemapBlock * kRemapQPT - 1) / ((long long)kRemapBlock * kRemapQPT);
     if (a.spitch < 4 * (cn == 1 ? 2 : 3) || b.spitch < 4 * (cn == 1 ? 2 : 3)) vec_src = false;  // rows too short for the aligned reads
     if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
     dim3 grid((unsigned)(per_job * n_jobs)), block(kRemapBlock);
