@@ -78,7 +78,10 @@ __device__ __forceinline__ void store_px4(uint8_t* p, const Px4& v, bool vec, in
 // compute, and the grid is sized to one sweep (~4 waves per SIMD at 1080p): the
 // row-by-row form with a fixed 256-block grid ran latency-bound.  When W % 4 == 0 and the rows are 4-byte aligned
 // every full sweep is straight-line vector code; the rest take a byte path.
-constexpr int kU = 2;
+#ifndef USV_PREP_KU
+#define USV_PREP_KU 2  // quads per thread per sweep (all their loads issued before any compute)
+#endif
+constexpr int kU = USV_PREP_KU;
 constexpr int kPT = USV_PREP_THREADS;  // threads per block (frame prep)
 static_assert(kPT % 256 == 0 && kPT <= 1024, "whole 256-bin groups of threads");
 

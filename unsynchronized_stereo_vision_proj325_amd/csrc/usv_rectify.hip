@@ -68,11 +68,13 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
 }
 
 // Quads (4 output pixels) over a flat, XCD-contiguous range per camera; remap_quad (usv_remap.hpp)
-// computes one, the result leaves as one 4-B (gray) or one 12-B (BGR) store.  A thread takes kRemapQPT
-// quads, a grid-stride apart, and has the NEXT quad's map words in flight while it gathers and blends
-// the current one: with one quad per thread every wave was a dependent map-load -> source-load ->
-// store chain, and the launch ran at two such chains' latency (without any source reads at all it
-// still took 11.4 of its 13.7 us; profiles/probes_r03/ab_remap_gather_r03.txt).
+// computes one, the result leaves as one 4-B (gray) or one 12-B (BGR) store.  With kRemapQPT > 1 a
+// thread takes that many quads a grid-stride apart and has the next quad's map words in flight while it
+// gathers and blends the current one.  Measured (profiles/probes_r03/ab_remap_gather_r03.txt): without
+// any source reads the one-quad kernel still took 11.4 of its 13.7 us, yet 2, 4 and 8 quads per thread
+// were slower (16.5 / 15.0 / 18.9 vs 15.2 us on one box): the launch is bound by its per-quad VALU
+// (~250 instructions: decode, clamps, two alignbytes and 3 x (2 v_perm + 2 v_dot2) per pixel, byte
+// packing) and wants every wave slot, not by the map round trip.  One quad per thread stays.
 #ifndef USV_REMAP_BLOCK
 #define USV_REMAP_BLOCK 256  // threads per block
 #endif
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
 #define USV_REMAP_XCD 1  // XCD-contiguous block order
 #endif
 #ifndef USV_REMAP_QPT
-#define USV_REMAP_QPT 4  // quads per thread (map prefetched one quad ahead)
+#define USV_REMAP_QPT 1  // quads per thread (> 1: map prefetched one quad ahead; measured slower)
 #endif
 constexpr int kRemapBlock = USV_REMAP_BLOCK;
 constexpr int kRemapQPT = USV_REMAP_QPT;
