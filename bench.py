@@ -177,45 +177,52 @@ def cpu_naive_configs() -> dict:
     return res
 
 
-def time_launches(fn, steps: int, stream, warm_ms: float = 10.0, graph_ok: bool = True) -> float:
+_BUSY = []
+
+
+def _busy_work(n: int, stream) -> None:
+    """Enqueue n full-chip elementwise passes over 64 MB (~20-30 us each): they hold the stream while the
+    host enqueues the timed launches behind them and keep the clocks up (a one-wave spin kernel let the
+    GPU lower them)."""
+    if not _BUSY:
+        _BUSY.extend([torch.zeros(16 << 20, dtype=torch.float32, device=stream.device) for _ in range(2)])
+    a, b = _BUSY
+    with torch.cuda.stream(stream):
+        for _ in range(n):
+            torch.add(a, 1.0, out=b)
+
+
+def time_launches(fn, steps: int, stream, warm_ms: float = 10.0, graph_ok: bool = True,
+                  preload: str = "busy") -> float:
     """Average duration (us) of `fn()` over `steps` back-to-back launches, HIP events on `stream`.
-    The launches are captured once into a HIP graph and replayed, so the interval is GPU time with no
-    host enqueue gaps (most of these kernels run shorter than one Python launch), after `warm_ms` of
-    untimed launches: the GPU lowers its clocks whenever it idles (a spin kernel ahead of the launches,
-    the round-2 method, let them drop: 62.2 vs 59.0 us per launch for config C).  Falls back to plain
-    back-to-back launches if the capture fails."""
+    After `warm_ms` of untimed launches (the GPU lowers its clocks whenever it idles) the stream is
+    preloaded so that the host's enqueue time is hidden, then the launches are enqueued between two
+    events: the interval is GPU time, without enqueue gaps or an idle-lowered clock.  preload "busy":
+    full-chip elementwise passes over 64 MB (for kernels shorter than a Python launch); "self": `steps`
+    untimed launches of fn itself (for kernels longer than a launch -- the matcher: memory-bound busy
+    work ahead of it let the core clock sag, 63.6 vs 56.8 us).  Round 2 held the stream with a one-wave
+    spin kernel, during which the clocks dropped (62.2 vs 59.0 us per launch at config C); a HIP-graph
+    replay adds ~5 us per node to few-us kernels."""
+    del graph_ok  # (kept for callers; no capture is used)
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    graph = None
-    try:
-        if not graph_ok:
-            raise RuntimeError("capture not wanted")
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            for _ in range(steps):
-                fn()
-        graph.replay()
-        torch.cuda.synchronize()
-    except RuntimeError:
-        graph = None
-        torch.cuda.synchronize()
     t_w = time.perf_counter()
     while (time.perf_counter() - t_w) * 1e3 < warm_ms:
-        if graph is not None:
-            graph.replay()
-        else:
-            for _ in range(steps):
-                fn()
+        for _ in range(8):
+            fn()
         torch.cuda.synchronize()
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(stream):
-        start.record(stream)
-        if graph is not None:
-            graph.replay()
-        else:
+    if preload == "self":
+        with torch.cuda.stream(stream):
             for _ in range(steps):
                 fn()
+    else:
+        _busy_work(max(8, steps), stream)  # >= ~25 us of GPU work per launch the host must enqueue
+    with torch.cuda.stream(stream):
+        start.record(stream)
+        for _ in range(steps):
+            fn()
         end.record(stream)
     end.synchronize()
     return start.elapsed_time(end) / steps * 1e3
@@ -436,7 +443,7 @@ def frame_chain_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
         pr(rect_r, *bufs[1])
         matcher.compute(bufs[0][2], bufs[1][2], with_distance=True, out_disp=disp, out_dist=dist)
 
-    us = time_launches(frame, steps, torch.cuda.current_stream())
+    us = time_launches(frame, steps, torch.cuda.current_stream(), preload="self")
     return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
             "stages": "rectify pair (BGR) -> frame prep x2 -> SAD w=%d D=%d -> distance map" % (w, D),
             "launches_per_frame": 1 + 2 * 2 + 1}
@@ -476,7 +483,7 @@ def frame_chain_fused_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> di
     gl = FramePrep(dev)(rect_l)[2]
     gr = FramePrep(dev)(rect_r)[2]
     same = bool(torch.equal(got, matcher.compute(gl, gr)))
-    us = time_launches(frame, steps, torch.cuda.current_stream())
+    us = time_launches(frame, steps, torch.cuda.current_stream(), preload="self")
     return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
             "stages": "rectify + HSV + hist (pair) -> equalize/HSV2BGR/gray (pair) -> SAD w=%d D=%d -> distance "
                       "map" % (w, D), "launches_per_frame": 3, "matches_six_launch_chain": same}
@@ -658,14 +665,14 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     d2 = torch.empty((H, 1918), dtype=torch.uint8, device=dev)
     Lc, Rc = Lt[:, :1918], Rt[:, :1918]
     ssd = StereoBlockMatcher(D, w, "ssd", kernel="fast")
-    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s)
+    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s, preload="self")
     out["ssd_fast"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
     for kernel, n in (("tiled", steps * 8), ("generic", steps)):
         ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)
-        us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s)
+        us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s, preload="self")
         out[f"ssd_{kernel}"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
         sad = StereoBlockMatcher(D, w, kernel=kernel)
-        us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s)
+        us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s, preload="self")
         out[f"sad_{kernel}_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
                                       "value": 1918 * H / (us * 1e-6)}
     out["note"] = "AUTO runs ssd_fast for SSD at 11 <= w <= 15 and the tiled kernel (vertical running sums, " \
@@ -806,7 +813,7 @@ def main():
         kern_ms = time_launches(lambda: matcher.compute(Lt, Rt, with_distance=with_dist,
                                                         out_disp=disp_bufs[0][0, :rows],
                                                         out_dist=dist_bufs[0] if with_dist else None),
-                                a.kernel_steps, stream) / 1e3
+                                a.kernel_steps, stream, preload="self") / 1e3
     else:
         kern_ms = span_ms
 

@@ -67,28 +67,35 @@ __global__ __launch_bounds__(64) void rectify_map_kernel(RectParams p, int W, in
     }
 }
 
-// Quads (4 output pixels) over a flat, XCD-contiguous range per camera; remap_quad (usv_remap.hpp)
-// computes one, the result leaves as one 4-B (gray) or one 12-B (BGR) store.  With kRemapQPT > 1 a
-// thread takes that many quads a grid-stride apart and has the next quad's map words in flight while it
-// gathers and blends the current one.  Measured (profiles/probes_r03/ab_remap_gather_r03.txt): without
-// any source reads the one-quad kernel still took 11.4 of its 13.7 us, yet 2, 4 and 8 quads per thread
-// were slower (16.5 / 15.0 / 18.9 vs 15.2 us on one box): the launch is bound by its per-quad VALU
-// (~250 instructions: decode, clamps, two alignbytes and 3 x (2 v_perm + 2 v_dot2) per pixel, byte
-// packing) and wants every wave slot, not by the map round trip.  One quad per thread stays.
+// One quad (4 output pixels) per thread over a flat, XCD-contiguous range of quads per camera;
+// remap_quad (usv_remap.hpp) computes it, the result leaves as one 4-B (gray) or one 12-B (BGR)
+// store.  Measured alternatives, all slower (profiles/probes_r03/ab_remap_gather_r03.txt): two or four
+// quads per thread with every load issued first (18.1 / 24.6 vs 15.1 us), and 2 / 4 / 8 quads per thread
+// with the next quad's map prefetched during the current quad's gathers (16.5 / 15.0 / 18.9 vs 15.2 us).
+// A build with no source reads at all still took 11.4 of 13.7 us: the launch is bound by its per-quad
+// VALU (~250 instructions: decode, clamps, alignbytes, 3 x (2 v_perm + 2 v_dot2) per pixel, packing)
+// and wants every wave slot, not by the map round trip.
 #ifndef USV_REMAP_BLOCK
 #define USV_REMAP_BLOCK 256  // threads per block
 #endif
 #ifndef USV_REMAP_XCD
 #define USV_REMAP_XCD 1  // XCD-contiguous block order
 #endif
-#ifndef USV_REMAP_QPT
-#define USV_REMAP_QPT 1  // quads per thread (> 1: map prefetched one quad ahead; measured slower)
-#endif
 constexpr int kRemapBlock = USV_REMAP_BLOCK;
-constexpr int kRemapQPT = USV_REMAP_QPT;
-template <int CN>
-__device__ __forceinline__ void remap_store(const RemapJob& j, int y, int x0, int n, int vec_dst,
-                                            const uint32_t (&out)[4 * CN]) {
+template <int CN, bool PK>
+__global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
+                                                    unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
+    const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const unsigned job = lb >= blocks_per_job ? 1u : 0u;
+    const RemapJob& j = job ? j1 : j0;
+    const unsigned nq = (unsigned)(W + 3) >> 2;
+    const unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
+    if (q >= nq * (unsigned)H) return;
+    const int y = (int)(q / nq);
+    const int x0 = 4 * (int)(q - (unsigned)y * nq);
+    const int n = min(4, W - x0);
+    uint32_t out[4 * CN];
+    remap_quad<CN, PK>(j, sW, sH, W, y, x0, n, vec_map, vec_src, out);
     uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
     if (vec_dst && n == 4) {
         if constexpr (CN == 3) {
@@ -102,40 +109,6 @@ __device__ __forceinline__ void remap_store(const RemapJob& j, int y, int x0, in
         }
     } else {
         for (int b = 0; b < n * CN; ++b) d[b] = (uint8_t)out[b];
-    }
-}
-template <int CN, bool PK>
-__global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
-                                                    unsigned blocks_per_job, int vec_map, int vec_dst, int vec_src) {
-    const unsigned lb = USV_REMAP_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const unsigned job = lb >= blocks_per_job ? 1u : 0u;
-    const RemapJob& j = job ? j1 : j0;
-    const unsigned nq = (unsigned)(W + 3) >> 2, total = nq * (unsigned)H;
-    const unsigned stride = blocks_per_job * (unsigned)kRemapBlock;
-    unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
-    if (q >= total) return;
-    auto where = [&](unsigned qq, int& y, int& x0, int& n) {
-        y = (int)(qq / nq);
-        x0 = 4 * (int)(qq - (unsigned)y * nq);
-        n = min(4, W - x0);
-    };
-    int y, x0, n;
-    where(q, y, x0, n);
-    RemapMapRaw next = remap_map_load<PK>(j, W, y, x0, n, vec_map);
-    for (;;) {
-        const RemapMapRaw cur = next;
-        const int cy = y, cx0 = x0, cn = n;
-        const unsigned qn = q + stride;
-        const bool more = qn < total;
-        if (more) {  // the next quad's map is in flight during this quad's gathers
-            where(qn, y, x0, n);
-            next = remap_map_load<PK>(j, W, y, x0, n, vec_map);
-        }
-        uint32_t out[4 * CN];
-        remap_quad_from<CN, PK>(j, cur, sW, sH, vec_src, out);
-        remap_store<CN>(j, cy, cx0, cn, vec_dst, out);
-        if (!more) break;
-        q = qn;
     }
 }
 
@@ -156,7 +129,7 @@ usv_status launch_remap(const RemapJob& a, const RemapJob& b, int n_jobs, int cn
         a.spitch >= (1 << 24) || b.spitch >= (1 << 24))
         return USV_ERR_UNSUPPORTED;
     const long long quads = (long long)((W + 3) / 4) * H;
-    const long long per_job = (quads + (long long)kRemapBlock * kRemapQPT - 1) / ((long long)kRemapBlock * kRemapQPT);
+    const long long per_job = (quads + kRemapBlock - 1) / kRemapBlock;
     if (a.spitch < 4 * (cn == 1 ? 2 : 3) || b.spitch < 4 * (cn == 1 ? 2 : 3)) vec_src = false;  // rows too short for the aligned reads
     if (per_job * n_jobs > 0x7FFFFFFFLL) return USV_ERR_UNSUPPORTED;
     dim3 grid((unsigned)(per_job * n_jobs)), block(kRemapBlock);

@@ -11,9 +11,6 @@
 #ifndef USV_REMAP_NT
 #define USV_REMAP_NT 0
 #endif
-#ifndef USV_REMAP_EXP
-#define USV_REMAP_EXP 0  // timing experiments only (wrong results): 1 no source reads, 2 one source read per row
-#endif
 
 namespace usv {
 
@@ -66,65 +63,54 @@ __device__ __forceinline__ unsigned xcd_block(unsigned lin, unsigned total) {
 //     two taps of a row are one u16 pair and their weights another: two v_dot2_u32_u16 per channel.
 //   * Source offsets are 32-bit (sy * pitch + byte, a 24-bit multiply: pitch < 2^24, checked by the
 //     launchers) from the job's base pointer.
-// The map words of one quad as they sit in memory: packed form (PK) w[0..3] = the four packed words;
-// map pair w[0..3] = the CV_16SC2 words (sx | sy << 16), w[4..5] = the CV_16UC1 pairs.  Loading them
-// is split from the rest of the quad so that a thread can have the NEXT quad's map in flight while it
-// gathers the current one's source pixels (remap_kernel).
-struct RemapMapRaw {
-    uint32_t w[6];
-};
-template <bool PK>
-__device__ __forceinline__ RemapMapRaw remap_map_load(const RemapJob& j, int W, int y, int x0, int n, int vec_map) {
-    RemapMapRaw r;
-    const size_t mrow = (size_t)y * W + x0;
-    if constexpr (PK) {  // one 16-B load for the quad's four packed words
-        if (vec_map && n == 4) {
-            const uint4 m = *reinterpret_cast<const uint4*>(j.pmap + mrow);
-            r.w[0] = m.x; r.w[1] = m.y; r.w[2] = m.z; r.w[3] = m.w;
-        } else {
-            for (int k = 0; k < 4; ++k) r.w[k] = j.pmap[mrow + (k < n ? k : 0)];
-        }
-        r.w[4] = r.w[5] = 0;
-    } else if (vec_map && n == 4) {
-#if USV_REMAP_NT  // the maps are read once per frame: non-temporal loads
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        typedef unsigned v2u __attribute__((ext_vector_type(2)));
-        const v4u av = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(j.map1 + 2 * mrow));
-        const v2u fv = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(j.map2 + mrow));
-        r.w[0] = av[0]; r.w[1] = av[1]; r.w[2] = av[2]; r.w[3] = av[3]; r.w[4] = fv[0]; r.w[5] = fv[1];
-#else
-        const uint4 a = *reinterpret_cast<const uint4*>(j.map1 + 2 * mrow);
-        const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
-        r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w; r.w[4] = f.x; r.w[5] = f.y;
-#endif
-    } else {
-        uint32_t f[4];
-        for (int k = 0; k < 4; ++k) {
-            const size_t kk = mrow + (k < n ? k : 0);
-            r.w[k] = (uint32_t)(uint16_t)j.map1[2 * kk] | ((uint32_t)(uint16_t)j.map1[2 * kk + 1] << 16);
-            f[k] = j.map2[kk];
-        }
-        r.w[4] = f[0] | (f[1] << 16);
-        r.w[5] = f[2] | (f[3] << 16);
-    }
-    return r;
-}
-
 template <int CN, bool PK = false>
-__device__ __forceinline__ void remap_quad_from(const RemapJob& j, const RemapMapRaw& raw, int sW, int sH,
-                                                int vec_src, uint32_t (&out)[4 * CN]) {
+__device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, int W, int y, int x0, int n,
+                                           int vec_map, int vec_src, uint32_t (&out)[4 * CN]) {
     constexpr int NWD = CN == 1 ? 2 : 3;
     int mx[4], my[4], mf[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if constexpr (PK) {
-            mf[k] = (int)(raw.w[k] & 1023u);
-            mx[k] = (int)((raw.w[k] >> 10) & 2047u) - 1;
-            my[k] = (int)(raw.w[k] >> 21) - 1;
+    const size_t mrow = (size_t)y * W + x0;
+    if constexpr (PK) {  // one 16-B load for the quad's four packed words
+        uint32_t w4[4];
+        if (vec_map && n == 4) {
+            const uint4 m = *reinterpret_cast<const uint4*>(j.pmap + mrow);
+            w4[0] = m.x; w4[1] = m.y; w4[2] = m.z; w4[3] = m.w;
         } else {
-            mx[k] = (int)(int16_t)(raw.w[k] & 0xFFFFu);
-            my[k] = (int)(int16_t)(raw.w[k] >> 16);
-            mf[k] = (int)((raw.w[4 + (k >> 1)] >> (16 * (k & 1))) & 0xFFFFu);
+            for (int k = 0; k < 4; ++k) w4[k] = j.pmap[mrow + (k < n ? k : 0)];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mf[k] = (int)(w4[k] & 1023u);
+            mx[k] = (int)((w4[k] >> 10) & 2047u) - 1;
+            my[k] = (int)(w4[k] >> 21) - 1;
+        }
+    } else if (vec_map && n == 4) {
+#if USV_REMAP_NT  // the maps are read once per frame: non-temporal loads
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        const v4i av = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(j.map1 + 2 * mrow));
+        const v2u fv = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(j.map2 + mrow));
+        const int4 a = make_int4(av[0], av[1], av[2], av[3]);
+        const uint2 f = make_uint2(fv[0], fv[1]);
+#else
+        const int4 a = *reinterpret_cast<const int4*>(j.map1 + 2 * mrow);
+        const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
+#endif
+        const int w4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mx[k] = (int)(int16_t)(w4[k] & 0xFFFF);
+            my[k] = (int)(int16_t)((unsigned)w4[k] >> 16);
+        }
+        mf[0] = f.x & 0xFFFF;
+        mf[1] = f.x >> 16;
+        mf[2] = f.y & 0xFFFF;
+        mf[3] = f.y >> 16;
+    } else {
+        for (int k = 0; k < 4; ++k) {
+            const int kk = k < n ? k : 0;
+            mx[k] = j.map1[2 * (mrow + kk)];
+            my[k] = j.map1[2 * (mrow + kk) + 1];
+            mf[k] = j.map2[mrow + kk];
         }
     }
     const int amax = (j.spitch - 4 * NWD) & ~3;
@@ -145,16 +131,6 @@ __device__ __forceinline__ void remap_quad_from(const RemapJob& j, const RemapMa
         const uint32_t r0 = __umul24((uint32_t)yc, (uint32_t)j.spitch) + (uint32_t)ac;
         const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
         const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r0 + (uint32_t)(sH > 1 ? j.spitch : 0));
-        if constexpr (USV_REMAP_EXP == 1) {
-#pragma unroll
-            for (int i = 0; i < NWD; ++i) u0[k][i] = u1[k][i] = r0 + i;
-            continue;
-        } else if constexpr (USV_REMAP_EXP == 2) {
-            const uint32_t w0 = q0[0], w1 = q1[0];
-#pragma unroll
-            for (int i = 0; i < NWD; ++i) { u0[k][i] = w0 + i; u1[k][i] = w1 + i; }
-            continue;
-        }
 #pragma unroll
         for (int i = 0; i < NWD; ++i) {
             u0[k][i] = q0[i];
@@ -203,12 +179,6 @@ __device__ __forceinline__ void remap_quad_from(const RemapJob& j, const RemapMa
             }
         }
     }
-}
-
-template <int CN, bool PK = false>
-__device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, int W, int y, int x0, int n,
-                                           int vec_map, int vec_src, uint32_t (&out)[4 * CN]) {
-    remap_quad_from<CN, PK>(j, remap_map_load<PK>(j, W, y, x0, n, vec_map), sW, sH, vec_src, out);
 }
 
 }  // namespace usv
