@@ -103,7 +103,7 @@ __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, int blk, 
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const unsigned q = (unsigned)(b + u * kPT);
-            y[u] = (int)(q / (unsigned)nq);
+            y[u] = (int)quad_row(q, (unsigned)nq, quad_row_fast((unsigned)Q, (unsigned)nq));
             x[u] = 4 * (int)(q - (unsigned)y[u] * (unsigned)nq);
             in[u] = load(y[u], x[u], 4, true);
         }
@@ -364,8 +364,9 @@ __global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, R
     if (blk == 0)
         for (int c = 0; c < kHistCopies; ++c) j.work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
     __syncthreads();
+    const bool fastq = quad_row_fast((unsigned)Q, (unsigned)nq);
     for (int q = blk * 256 + t; q < Q; q += blocks_per_job * 256) {
-        const int y = q / nq, x0 = 4 * (q - y * nq), n = min(4, W - x0);
+        const int y = (int)quad_row((unsigned)q, (unsigned)nq, fastq), x0 = 4 * (q - y * nq), n = min(4, W - x0);
         uint32_t px[12];
         remap_quad<3, PK>(j.r, sW, sH, W, y, x0, n, vec_map, vec_src, px);
         Px4 out;

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kRemapBlock) void remap_kernel(RemapJob j0, RemapJo
     const unsigned nq = (unsigned)(W + 3) >> 2;
     const unsigned q = (lb - job * blocks_per_job) * (unsigned)kRemapBlock + threadIdx.x;
     if (q >= nq * (unsigned)H) return;
-    const int y = (int)(q / nq);
+    const int y = (int)quad_row(q, nq, quad_row_fast(nq * (unsigned)H, nq));
     const int x0 = 4 * (int)(q - (unsigned)y * nq);
     const int n = min(4, W - x0);
     uint32_t out[4 * CN];

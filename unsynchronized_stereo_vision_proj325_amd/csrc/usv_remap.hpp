@@ -11,6 +11,9 @@
 #ifndef USV_REMAP_NT
 #define USV_REMAP_NT 0
 #endif
+#ifndef USV_REMAP_BUF
+#define USV_REMAP_BUF 1  // source reads as raw-buffer loads: 32-bit offsets, no 64-bit address arithmetic
+#endif
 
 namespace usv {
 
@@ -42,6 +45,20 @@ __host__ __device__ __forceinline__ uint32_t pack_map_word(int sx, int sy, int f
 typedef unsigned short remap_us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t remap_dot2(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(remap_us2, a), __builtin_bit_cast(remap_us2, b), c, false);
+}
+
+// q / d for a quad index q and the quads per row d (both wave-uniform d): through the f32 reciprocal when
+// q < 2^24 and d >= 8 -- the f32 quotient is then within one of the true one and a single correction makes
+// it exact -- instead of the ~15-instruction integer division sequence; plain division otherwise.
+__device__ __forceinline__ unsigned quad_row(unsigned q, unsigned d, bool fast) {
+    if (!fast) return q / d;
+    unsigned y = (unsigned)((float)q * __builtin_amdgcn_rcpf((float)d));
+    const int r = (int)(q - y * d);
+    y = r < 0 ? y - 1u : (r >= (int)d ? y + 1u : y);
+    return y;
+}
+__host__ __device__ __forceinline__ bool quad_row_fast(unsigned total_quads, unsigned d) {
+    return total_quads < (1u << 24) && d >= 8u;
 }
 
 // Block b of a launch runs on XCD b % 8; the logical block number that gives XCD k the k-th
@@ -129,13 +146,27 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
         const bool in = sx >= 0 && sx + 1 < sW && sy >= 0 && sy + 1 < sH && a == ac;
         good |= in ? 1u << k : 0u;
         const uint32_t r0 = __umul24((uint32_t)yc, (uint32_t)j.spitch) + (uint32_t)ac;
+        const uint32_t r1 = r0 + (uint32_t)(sH > 1 ? j.spitch : 0);
+#if USV_REMAP_BUF
+        // a raw buffer over the source (stride 0, no range limit: the offsets stay inside the image): each
+        // read is a 32-bit VGPR offset with the dword index in the instruction's immediate offset, instead
+        // of a 64-bit address built per read
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(j.src), (short)0, (int)0xFFFFFFFF, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < NWD; ++i) {
+            u0[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r0 + 4u * (uint32_t)i, 0, 0);
+            u1[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r1 + 4u * (uint32_t)i, 0, 0);
+        }
+#else
         const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r0 + (uint32_t)(sH > 1 ? j.spitch : 0));
+        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r1);
 #pragma unroll
         for (int i = 0; i < NWD; ++i) {
             u0[k][i] = q0[i];
             u1[k][i] = q1[i];
         }
+#endif
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
