@@ -767,20 +767,31 @@ def main():
             else:
                 pending[b] = work
 
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
     for i in range(a.warmup):
         step(i)
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+    torch.cuda.synchronize()
+    per_step_s = (time.perf_counter() - t_w) / max(1, a.warmup)
     # Clock warm-up (untimed): from idle the MI355X runs the first ~20 ms of back-to-back launches at
     # lower clocks -- config C's kernel took 82.5 us per launch in a first 200-launch pass and 58.3 us in
     # the next (scripts/exp_launch.py, profiles/probes_r03/launch_modes_r03.txt).  A throughput number is
-    # a sustained-load number, so the timed region starts after --warm-ms of the same steps.
-    warm_steps = 0
-    if a.warm_ms > 0:
-        t_w = time.perf_counter()
-        while (time.perf_counter() - t_w) * 1e3 < a.warm_ms and warm_steps < 20000:
-            for _ in range(8):
-                step(a.warmup + warm_steps)
-                warm_steps += 1
-            torch.cuda.synchronize()
+    # a sustained-load number, so the timed region starts after about --warm-ms of the same steps.  The
+    # step count comes from the W warm-up steps' pace and is the same on every rank (MAX over ranks):
+    # each step may carry a collective.
+    warm_steps = int(min(20000, a.warm_ms * 1e-3 / max(per_step_s, 1e-6))) if a.warm_ms > 0 else 0
+    if world > 1:
+        t = torch.tensor([warm_steps], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        warm_steps = int(t.item())
+    for i in range(warm_steps):
+        step(a.warmup + i)
+        if i % 64 == 63:
+            torch.cuda.synchronize()  # (bounded queue depth)
     for b in range(nbuf):
         if pending[b] is not None:
             pending[b].wait()

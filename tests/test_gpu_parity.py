@@ -213,6 +213,19 @@ def test_group_kernel_pitched_outputs(gpu, D, w, dcol, dcol_dist, dist_pitch):
     assert (bf[outside] == -1.0).all()
 
 
+def test_group_kernel_pitched_inputs(gpu):
+    """Group kernel on views of larger buffers (row pitch 300, 4-aligned column offset): the L and R row
+    DMAs use the pitch, the replicate border the view's own columns."""
+    rng = np.random.default_rng(21)
+    big_L = torch.from_numpy(rng.integers(0, 256, (70, 300), dtype=np.uint8)).to(gpu)
+    big_R = torch.from_numpy(rng.integers(0, 256, (70, 300), dtype=np.uint8)).to(gpu)
+    for D, w in ((48, 7), (30, 5), (64, 9)):
+        Lv, Rv = big_L[3:63, 8:208], big_R[3:63, 8:208]
+        got = StereoBlockMatcher(D, w, kernel="fast").compute(Lv, Rv).cpu().numpy()
+        ref = oracle_sad(Lv.cpu().numpy(), Rv.cpu().numpy(), D, w, "sad", "naive")
+        assert np.array_equal(got, ref), (D, w, _mismatch(got, ref))
+
+
 def test_group_kernel_batch(gpu):
     """Batched launch through the group kernel (pairs back to back, one launch)."""
     D, w, W, H = 48, 7, 320, 90

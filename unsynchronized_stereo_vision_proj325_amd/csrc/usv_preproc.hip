@@ -45,32 +45,43 @@ constexpr int kWHist = 0, kHistCopies = 8, kParityWords = 256 * kHistCopies;
 // 4 interleaved BGR / HSV pixels = 12 bytes = one dwordx3 when the row and x
 // are 4-pixel aligned; byte access otherwise.
 struct Px4 { int c[12]; };
-__device__ __forceinline__ Px4 load_px4(const uint8_t* p, bool vec, int n) {
+// Vector path: raw-buffer loads / stores over the image (32-bit offsets y * pitch + 3x, the dword index in
+// no register at all) instead of a 64-bit address per quad; the host only sets `vec` when every
+// pitch * H < 2^31.  Byte path: size_t pointer arithmetic.
+typedef unsigned px_v3u __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t px_rsrc(const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ Px4 load_px4(const uint8_t* base, int pitch, int y, int x, bool vec, int n) {
     Px4 r;
     if (vec) {
-        const uint3 w = *reinterpret_cast<const uint3*>(p);
+        const px_v3u w = __builtin_amdgcn_raw_buffer_load_b96(px_rsrc(base), (uint32_t)(y * pitch + 3 * x), 0, 0);
         const uint32_t ww[3] = {w.x, w.y, w.z};
 #pragma unroll
         for (int i = 0; i < 12; ++i) r.c[i] = (ww[i >> 2] >> (8 * (i & 3))) & 0xFF;
     } else {
+        const uint8_t* p = base + (size_t)y * pitch + 3 * (size_t)x;
 #pragma unroll
         for (int i = 0; i < 12; ++i) r.c[i] = i < 3 * n ? p[i] : 0;
     }
     return r;
 }
-__device__ __forceinline__ void store_px4(uint8_t* p, const Px4& v, bool vec, int n) {
+__device__ __forceinline__ void store_px4(uint8_t* base, int pitch, int y, int x, const Px4& v, bool vec, int n) {
     if (vec) {
-        uint3 w;
+        px_v3u w;
         w.x = v.c[0] | (v.c[1] << 8) | (v.c[2] << 16) | ((uint32_t)v.c[3] << 24);
         w.y = v.c[4] | (v.c[5] << 8) | (v.c[6] << 16) | ((uint32_t)v.c[7] << 24);
         w.z = v.c[8] | (v.c[9] << 8) | (v.c[10] << 16) | ((uint32_t)v.c[11] << 24);
-        *reinterpret_cast<uint3*>(p) = w;
+        __builtin_amdgcn_raw_buffer_store_b96(w, px_rsrc(base), (uint32_t)(y * pitch + 3 * x), 0, 0);
     } else {
+        uint8_t* p = base + (size_t)y * pitch + 3 * (size_t)x;
 #pragma unroll
         for (int i = 0; i < 12; ++i)  // static indices: a dynamic one would put the array in scratch
             if (i < 3 * n) p[i] = (uint8_t)v.c[i];
     }
 }
+// host: 32-bit buffer offsets cover every row of an image of H rows at this pitch
+static bool fits32(int pitch, int H) { return (long long)pitch * H < (1LL << 31); }
 
 // Pixels are processed as quads (4 interleaved pixels, one dwordx3) over the
 // whole image as one flat range: quad q -> row q / nq, column 4 (q % nq).  A
@@ -155,7 +166,7 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
         W, H, vec4, blk, blocks_per_job,
-        [&](int y, int x, int n, bool v) { return load_px4(bgr + (size_t)y * pitch + 3 * x, v, n); },
+        [&](int y, int x, int n, bool v) { return load_px4(bgr, pitch, y, x, v, n); },
         [&] {
             hsv_tables(sdiv, hdiv);
             for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
@@ -174,7 +185,7 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
                 out.c[3 * k + 2] = val;
                 if (!(USV_PREP_EXP & 2) && k < n) atomicAdd(&lh[wv][val], 1u);
             }
-            store_px4(hsv + (size_t)y * hsv_pitch + 3 * x, out, v, n);
+            store_px4(hsv, hsv_pitch, y, x, out, v, n);
         });
     __syncthreads();
     if (t < 256) {
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(kPT) void v_hist_kernel(HistJob j0, HistJob j1, int
     const bool vec4 = vec && (W & 3) == 0;
     for_each_quad(
         W, H, vec4, blk, blocks_per_job,
-        [&](int y, int x, int n, bool v) { return load_px4(j.bgr + (size_t)y * j.pitch + 3 * x, v, n); },
+        [&](int y, int x, int n, bool v) { return load_px4(j.bgr, j.pitch, y, x, v, n); },
         [&] {
             for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
             if (blk == 0 && t < 256)
@@ -301,8 +312,8 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
     for_each_quad(
         W, H, vec4, (int)blockIdx.x - job * blocks_per_job, blocks_per_job,
         [&](int y, int x, int n, bool v) {
-            if constexpr (FROM_BGR) return load_px4(j.src + (size_t)y * j.src_pitch + 3 * x, v, n);
-            else return load_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, v, n);
+            if constexpr (FROM_BGR) return load_px4(j.src, j.src_pitch, y, x, v, n);
+            else return load_px4(j.hsv, j.hsv_pitch, y, x, v, n);
         },
         build_lut,
         [&](int y, int x, int n, bool v, Px4 in) {
@@ -329,8 +340,8 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
                 o.c[3 * k + 2] = r;
                 g4 |= (uint32_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14) << (8 * k);
             }
-            store_px4(j.hsv + (size_t)y * j.hsv_pitch + 3 * x, in, v, n);
-            store_px4(j.bgr + (size_t)y * j.bgr_pitch + 3 * x, o, v, n);
+            store_px4(j.hsv, j.hsv_pitch, y, x, in, v, n);
+            store_px4(j.bgr, j.bgr_pitch, y, x, o, v, n);
             uint8_t* go = j.gray + (size_t)y * j.gray_pitch + x;
             if (v) *reinterpret_cast<uint32_t*>(go) = g4;
             else for (int k = 0; k < n; ++k) go[k] = (uint8_t)(g4 >> (8 * k));
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, R
             out.c[3 * k + 2] = val;
             if (k < n) atomicAdd(&lh[wv][val], 1u);
         }
-        store_px4(j.r.dst + (size_t)y * j.r.dpitch + 3 * x0, out, vec_dst && n == 4, n);
+        store_px4(j.r.dst, j.r.dpitch, y, x0, out, vec_dst && n == 4, n);
     }
     __syncthreads();
     const uint32_t sum = lh[0][t] + lh[1][t] + lh[2][t] + lh[3][t];
@@ -520,7 +531,8 @@ usv_status usv_bgr2hsv_hist_u8(const uint8_t* bgr, int W, int H, int pitch, uint
     if (!bgr || !hsv || !work || W <= 0 || H <= 0 || pitch < 3 * W || hsv_pitch < 3 * W ||
         (long long)W * H > (1LL << 24) || !al4(work) || (parity != 0 && parity != 1))
         return USV_ERR_INVALID_ARG;
-    const int vec = al4(bgr) && al4(hsv) && pitch % 4 == 0 && hsv_pitch % 4 == 0;
+    const int vec = al4(bgr) && al4(hsv) && pitch % 4 == 0 && hsv_pitch % 4 == 0 && usv::fits32(pitch, H) &&
+                    usv::fits32(hsv_pitch, H);
     const usv::HistJob j{bgr, pitch, hsv, hsv_pitch, static_cast<uint32_t*>(work)};
     const int nb = usv::prep_blocks(W, H);
     hipLaunchKernelGGL(usv::hsv_hist_kernel, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j, W, H,
@@ -535,7 +547,7 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
         gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) || (long long)W * H > (1LL << 24))
         return USV_ERR_INVALID_ARG;
     const int vec = al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
-                    gray_pitch % 4 == 0;
+                    gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) && usv::fits32(bgr_pitch, H);
     const usv::EqJob j{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch};
     const int nb = usv::prep_blocks(W, H);
     hipLaunchKernelGGL(usv::equalize_kernel<false>, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j,
@@ -551,9 +563,9 @@ usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_
         bgr_pitch < 3 * W || gray_pitch < W || !al4(work) || (parity != 0 && parity != 1) ||
         (long long)W * H > (1LL << 24))
         return USV_ERR_INVALID_ARG;
-    const int vh = al4(bgr) && pitch % 4 == 0;
+    const int vh = al4(bgr) && pitch % 4 == 0 && usv::fits32(pitch, H);
     const int ve = vh && al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
-                   gray_pitch % 4 == 0;
+                   gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) && usv::fits32(bgr_pitch, H);
     const usv::HistJob hj{bgr, pitch, nullptr, 0, static_cast<uint32_t*>(work)};
     const int nb = usv::prep_blocks(W, H);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -576,9 +588,10 @@ usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int 
     uint32_t* wL = static_cast<uint32_t*>(work);
     uint32_t* wR = wL + USV_FRAME_PREP_WORK_BYTES / 4;
     // V histograms (reads only), then BGR2HSV + equalize + HSV2BGR + gray from the BGR frames
-    const int vh = al4(bgrL) && al4(bgrR) && pitch % 4 == 0;
+    const int vh = al4(bgrL) && al4(bgrR) && pitch % 4 == 0 && usv::fits32(pitch, H);
     const int ve = vh && al4(hsvL) && al4(hsvR) && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) &&
-                   hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 && gray_pitch % 4 == 0;
+                   hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 && gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) &&
+                   usv::fits32(bgr_pitch, H);
     const int nb = usv::prep_blocks(W, H);
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, nullptr, 0, wL},
@@ -612,9 +625,9 @@ static usv_status rectify_prep_pair(const usv::RemapJob& jl_r, const usv::RemapJ
                                             : al(jl_r.map1, 16) && al(jr_r.map1, 16) && al(jl_r.map2, 8) &&
                                                   al(jr_r.map2, 8));
     const int vec_src = al4(jl_r.src) && al4(jr_r.src) && spitch % 4 == 0 && spitch >= 12;
-    const int vec_hsv = al4(hsvL) && al4(hsvR) && hsv_pitch % 4 == 0;
+    const int vec_hsv = al4(hsvL) && al4(hsvR) && hsv_pitch % 4 == 0 && usv::fits32(hsv_pitch, H);
     const int ve = vec_hsv && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) && bgr_pitch % 4 == 0 &&
-                   gray_pitch % 4 == 0;
+                   gray_pitch % 4 == 0 && usv::fits32(bgr_pitch, H);
     // rectify + HSV + histogram: a quad per thread per iteration, ~4 quads per thread at 1080p
     const long long quads = (long long)((W + 3) / 4) * H;
     const int per_job = (int)std::max<long long>(1, std::min<long long>(1024, (quads + 1023) / 1024));
