@@ -776,7 +776,16 @@ def main():
             pending[b].wait()
             pending[b] = None
     torch.cuda.synchronize()
-    per_step_s = (time.perf_counter() - t_w) / max(1, a.warmup)
+    # pace of a step, from 16 more untimed steps (the W steps include first-launch costs)
+    t_w = time.perf_counter()
+    for i in range(16):
+        step(a.warmup + i)
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+    torch.cuda.synchronize()
+    per_step_s = (time.perf_counter() - t_w) / 16
     # Clock warm-up (untimed): from idle the MI355X runs the first ~20 ms of back-to-back launches at
     # lower clocks -- config C's kernel took 82.5 us per launch in a first 200-launch pass and 58.3 us in
     # the next (scripts/exp_launch.py, profiles/probes_r03/launch_modes_r03.txt).  A throughput number is
@@ -789,7 +798,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         warm_steps = int(t.item())
     for i in range(warm_steps):
-        step(a.warmup + i)
+        step(a.warmup + 16 + i)
         if i % 64 == 63:
             torch.cuda.synchronize()  # (bounded queue depth)
     for b in range(nbuf):
