@@ -1069,6 +1069,9 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 #ifndef USV_PAIR_PIPE
 #define USV_PAIR_PIPE 1  // argmin transpose of row t finished during row t + 1 (latency hidden by the chain)
 #endif
+#ifndef USV_NT_DIST
+#define USV_NT_DIST 0  // experiment: the paired kernel's distance map through non-temporal stores
+#endif
 #ifndef USV_WIDE_FLUSH
 #define USV_WIDE_FLUSH 1  // paired kernel: one 8-byte disparity store and one 16-byte distance store per lane per chunk
 #endif
@@ -1361,7 +1364,13 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 }
                 const size_t y = (size_t)(y_chunk + r);
                 if (!(USV_PEXP == 10 && y != 0x7FFFFFFF))
-                    *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+                    if constexpr (USV_NT_DIST) {  // experiment: write-once map as non-temporal stores
+                        typedef double v2d __attribute__((ext_vector_type(2)));
+                        v2d v = {lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+                        __builtin_nontemporal_store(v, reinterpret_cast<v2d*>(dist + y * a.dist_pitch + x0 + 2 * q));
+                    } else {
+                        *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+                    }
             }
             y_chunk += rows;
             cb ^= 1;
