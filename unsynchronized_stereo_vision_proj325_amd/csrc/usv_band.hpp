@@ -21,7 +21,7 @@ struct BandSpan {
 // Band s of the column whose band sb is carried by tile t(sb) = t0 + sb * nxt (t0 = pair * per_pair +
 // col_xt); tiles run XCD-contiguously: runs of long_run tiles up to tile `split`, then runs of `base`.
 // Generation of a tile = min(position in its run / gen_g, 3), weight = byte g of weights.
-__device__ __forceinline__ BandSpan band_span(unsigned pair, unsigned per_pair, unsigned nxt, unsigned col_xt,
+__host__ __device__ __forceinline__ BandSpan band_span(unsigned pair, unsigned per_pair, unsigned nxt, unsigned col_xt,
                                               unsigned s, unsigned m_col, unsigned base, unsigned long_run,
                                               unsigned split, unsigned gen_g, unsigned weights) {
     if (weights == 0x01010101u) return BandSpan{s, 1u, m_col};  // equal heights
