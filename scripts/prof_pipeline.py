@@ -20,7 +20,7 @@ prep = FramePrep(dev)
 gray = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
 prev = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
 pair = FramePrepPair(dev)
-for _ in range(20):
+for _ in range(int(os.environ.get("PP_ITERS", "20"))):
     ol, orr = rectify_pair(rl, rr, src[0], src[1])
     hsv, bgr, g = prep(ol)
     m, _ = ABSDiffSearch(gray, prev)
