@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="CPU-baseline sample budget: warm-up + 5 timed runs share it (N=1 only)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the oracle parity checks after the timed region (profiling passes only)")
     p.add_argument("--extra-steps", type=int, default=20,
                    help="timed frames per extra leg (end-to-end, frame chain, generic fallbacks); 0 = skip")
     p.add_argument("--warm-ms", type=float, default=60.0,
@@ -72,8 +74,8 @@ def parse():
                         "the GPU raises its clocks only under sustained load (0 = off)")
     p.add_argument("--kernel-steps", type=int, default=50,
                    help="launches of the separate back-to-back pass after the timed region that gives "
-                        "kernel_ms (HIP events around the pass only, a spin kernel ahead so the host enqueues "
-                        "them all); 0 = use the timed region's span")
+                        "kernel_ms (HIP events around the pass only, queued behind as many untimed launches "
+                        "so the host enqueues them all); 0 = use the timed region's span")
     p.add_argument("--pipeline-steps", type=int, default=50,
                    help="timed launches per pipeline leg (rectify / frame prep / mask); 0 = skip")
     return p.parse_args()
@@ -149,6 +151,77 @@ def cpu_baseline(L: np.ndarray, R: np.ndarray, D: int, w: int, budget_s: float, 
                   f"run ({reps * rows * W} output pixels per run), median of {runs} runs after one warm-up",
         "runs_s": times,
     }
+
+
+def _oracle_dist_lut(lib) -> np.ndarray:
+    """The oracle's 256-entry distance table (oracle/distance_oracle.c, P/DistanceCalculator.cpp:84)."""
+    return np.array([lib.usv_oracle_distance_cm(d) for d in range(256)], dtype=np.float64)
+
+
+def _mismatches(got_disp: np.ndarray, ref: np.ndarray, got_dist, lut: np.ndarray) -> dict:
+    """Mismatch counts of one output against the oracle's disparity map: u8 disparity bytes, and the f64
+    distance map bit for bit against lut[ref] (inf at d = 0 compares equal as bits)."""
+    res = {"pixels": int(ref.size), "disparity_mismatches": int((got_disp != ref).sum())}
+    if got_dist is not None:
+        want = lut[ref.astype(np.int64)]
+        res["distance_mismatches"] = int((got_dist.view(np.uint64) != want.view(np.uint64)).sum())
+    return res
+
+
+def parity_checks(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, outputs, one_shots: bool) -> dict:
+    """Checker, run after the timed region (never inside it): the timed kernel's own output buffers
+    against the oracle (oracle/sad_oracle.c sliding variant, bit-exact with the naive definition) on
+    the same pair, plus, with one_shots, full-size configs A, B, E and config C SSD through
+    StereoBlockMatcher and config D (batch of 8) through the C-ABI sharded engine (usv_batch_sharded,
+    one GPU).  Distance maps are compared bit for bit with the oracle's table at the oracle's
+    disparity (P/DistanceCalculator.cpp:84).  Returns per-config mismatch counts; "ok" is the AND."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_oracle, oracle_sad
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    lib = load_oracle()
+    lut = _oracle_dist_lut(lib)
+    H, W = L.shape
+    t0 = time.perf_counter()
+    ref = oracle_sad(L, R, D, w, "sad", "sliding", threads)
+    res = {}
+    for i, (disp_t, dist_t) in enumerate(outputs):
+        got = disp_t.cpu().numpy()
+        res[f"timed_buffer{i}"] = _mismatches(got, ref, dist_t.cpu().numpy() if dist_t is not None else None, lut)
+    if one_shots:
+        for name, (cW, cH, cD, cw, metric) in {"A": (320, 240, 32, 5, "sad"), "B": (640, 480, 64, 7, "sad"),
+                                              "C_ssd": (W, H, D, w, "ssd"),
+                                              "E": (3840, 2160, 256, 15, "sad")}.items():
+            cL, cR, _ = synthetic_pair(cW, cH, cD, pair_index=3, noise=2)
+            m = StereoBlockMatcher(cD, cw, metric)
+            disp, dist_map = m.compute(torch.from_numpy(cL).to(dev), torch.from_numpy(cR).to(dev), with_distance=True)
+            torch.cuda.synchronize()
+            cref = oracle_sad(cL, cR, cD, cw, metric, "sliding", threads)
+            res[name] = {"workload": f"{cW}x{cH} w={cw} D={cD} {metric.upper()}",
+                         **_mismatches(disp.cpu().numpy(), cref, dist_map.cpu().numpy(), lut)}
+            del disp, dist_map
+        from unsynchronized_stereo_vision_proj325_amd.sharding import ShardedMatcher
+        B = 8
+        pairs = [synthetic_pair(W, H, D, pair_index=16 + i, noise=2) for i in range(B)]
+        bL = np.stack([p[0] for p in pairs])
+        bR = np.stack([p[1] for p in pairs])
+        eng = ShardedMatcher([dev.index if dev.index is not None else 0], B, W, H, D, w)
+        try:
+            bd, bx = eng.run(bL, bR, with_distance=True)
+        finally:
+            eng.close()
+        tot = {"pixels": 0, "disparity_mismatches": 0, "distance_mismatches": 0}
+        for i in range(B):
+            mm = _mismatches(bd[i], oracle_sad(bL[i], bR[i], D, w, "sad", "sliding", threads), bx[i], lut)
+            for k in tot:
+                tot[k] += mm[k]
+        res["D"] = {"workload": f"batch of {B} x {W}x{H} w={w} D={D} SAD through usv_batch_sharded (1 GPU)", **tot}
+    bad = sum(v.get("disparity_mismatches", 0) + v.get("distance_mismatches", 0) for v in res.values())
+    res["ok"] = bad == 0
+    res["checker"] = (f"oracle/sad_oracle.c sliding variant ({threads} threads) and oracle/distance_oracle.c "
+                      "table; outside the timed region")
+    res["check_s"] = time.perf_counter() - t0
+    return res
 
 
 def cpu_naive_configs() -> dict:
@@ -842,6 +915,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
 
+    # Parity (outside the timed region): every rank checks the buffers its timed steps wrote against
+    # the oracle on the same input rows; rank 0 at N = 1 adds the one-shot configs A, B, C-SSD, D, E.
+    parity = None
+    if not a.no_parity:
+        torch.cuda.synchronize()
+        parity = parity_checks(dev, L[i0:i1], R[i0:i1], D, w,
+                               [(disp_bufs[b][0, :rows], dist_bufs[b] if with_dist else None) for b in range(nbuf)],
+                               one_shots=(world == 1 and rank == 0))
+        bad = torch.tensor([0 if parity["ok"] else 1], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+        parity["ranks_with_mismatches"] = int(bad.item())
+        parity["ok"] = parity["ranks_with_mismatches"] == 0
+
     pixels = W * H
     # bands: the job is one frame per step whatever N is; pairs: one frame per GPU per step
     value = (1 if bands else world) * a.steps * pixels / elapsed
@@ -876,8 +963,9 @@ def main():
         },
         "disparity_evals_per_s": value * D,
         "kernel_ms": kern_ms,
-        "kernel_timing": (f"HIP events around {a.kernel_steps} back-to-back launches after the timed region "
-                          "(a spin kernel holds the stream while the host enqueues them), kernel's stream"
+        "kernel_timing": (f"HIP events around {a.kernel_steps} back-to-back launches after the timed region, "
+                          f"enqueued behind {a.kernel_steps} untimed launches of the same kernel (so the host's "
+                          "enqueue time is hidden) after 10 ms of warm launches, kernel's stream"
                           if a.kernel_steps > 0 else "HIP events around the timed region, span / steps"),
         "span_ms_per_step": span_ms,
         "roofline": {
@@ -921,10 +1009,16 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(L, R, D, w, a.cpu_seconds)
         rec["cpu_baseline"]["speedup"] = value / rec["cpu_baseline"]["value"]
         rec["cpu_naive"] = cpu_naive_configs()
+    if parity is not None:
+        rec["parity"] = parity
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and not parity["ok"]:
+        print("bench.py: PARITY FAILURE -- the timed kernel's output differs from the oracle "
+              f"({json.dumps(parity)})", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -166,7 +166,9 @@ usv_status usv_sharded_destroy(usv_sharded_engine* e);
 
 /* DEVICE buffers of GPU k's shard inputs for the NEXT submit (dense, pitch W, pair j at j*W*H;
  * the engine alternates two buffer slots per GPU): fill them and pass L = R = NULL to
- * usv_batch_sharded(_submit) to match HBM-resident frames. */
+ * usv_batch_sharded(_submit) to match HBM-resident frames.  If that slot still holds a batch in
+ * flight, this call completes it first (as a submit on a busy slot does), so the buffers returned
+ * are never read by a running batch; that batch's status is reported by its own wait. */
 usv_status usv_sharded_input_buffers(usv_sharded_engine* e, int k, uint8_t** L, uint8_t** R);
 
 /* DEVICE results on devices[0] of the last COMPLETED batch: the gather buffer
@@ -188,10 +190,13 @@ usv_status usv_batch_sharded(usv_sharded_engine* e, const uint8_t* L, const uint
                              size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
                              const double* lut_cm, int with_distance);
 /* The same in two halves, two batches in flight: submit enqueues a batch on the next of two buffer
- * slots (host inputs are read before it returns; a submit while both slots are busy first completes
- * the older batch) and returns *ticket; wait completes that batch (disp / dist_cm filled).  Batch
- * k+1's copies and kernels overlap batch k's gather, distance expansion and D2H.  The host output
- * buffers of a batch must stay valid until its wait. */
+ * slots and returns *ticket; wait completes that batch (disp / dist_cm filled).  Host inputs (even
+ * pageable ones) have been copied when submit returns: the caller may reuse them at once.  A submit
+ * (or usv_sharded_input_buffers) that needs a busy slot first completes the older batch there -- its
+ * results are delivered, and the wait on its ticket then returns that completion's status (USV_OK,
+ * or the error it hit) once; a ticket never submitted or already waited for is USV_ERR_INVALID_ARG.
+ * Batch k+1's copies and kernels overlap batch k's gather, distance expansion and D2H.  The host
+ * output buffers of a batch must stay valid until its wait (or its implicit completion). */
 usv_status usv_batch_sharded_submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int batch,
                                     size_t pair_stride, int pitch, uint8_t* disp, double* dist_cm,
                                     const double* lut_cm, int with_distance, long long* ticket);

@@ -45,3 +45,23 @@ def test_world_size_mismatch_fails():
     out = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0",
                USV_BENCH_PLUMBING="1")
     assert out.returncode != 0 and "WORLD_SIZE" in (out.stderr + out.stdout)
+
+
+def test_parity_mismatch_counts():
+    """bench.py's parity checker counts disparity bytes and distance bits that differ from the oracle's
+    (inf at d = 0 compares equal as bits; a NaN or a 1-ulp change counts)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    lut = np.array([np.inf] + [1000.0 / d for d in range(1, 256)])
+    ref = np.array([[0, 1, 2], [3, 255, 0]], dtype=np.uint8)
+    got = ref.copy()
+    dist = lut[ref]
+    assert bench._mismatches(got, ref, dist, lut) == {"pixels": 6, "disparity_mismatches": 0, "distance_mismatches": 0}
+    got[0, 1] = 2
+    dist2 = dist.copy()
+    dist2[1, 1] = np.nextafter(dist2[1, 1], 0)
+    dist2[0, 0] = np.nan
+    assert bench._mismatches(got, ref, dist2, lut) == {"pixels": 6, "disparity_mismatches": 1,
+                                                        "distance_mismatches": 2}
+    assert bench._mismatches(got, ref, None, lut) == {"pixels": 6, "disparity_mismatches": 1}

@@ -143,10 +143,11 @@ def test_batch_sharded_two_batches_in_flight(gpu):
         lut = distance_lut_cm()
         for b, (h, bt) in enumerate(zip(hs, batches)):
             if b == 0:
-                # the third submit reused batch 0's slot: it completed batch 0 itself, so its ticket is gone
+                # the third submit reused batch 0's slot and completed batch 0 itself: its results are in
+                # place and its wait reports that completion's status (once)
+                disp, _ = eng.wait(h)
                 with pytest.raises(_lib.UsvError):
                     eng.wait(h)
-                disp = h["disp"]
             else:
                 disp, dist = eng.wait(h)
                 if b == 1:
@@ -155,3 +156,44 @@ def test_batch_sharded_two_batches_in_flight(gpu):
                 assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), (b, i)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_batch_sharded_resident_inputs_with_batch_in_flight(gpu):
+    """usv_sharded_input_buffers while the slot it hands out still holds a batch in flight: the engine
+    completes that batch first (delivered, its wait returns OK), so refilling the buffers for the next
+    resident batch cannot race with it; both batches bit-exact vs the oracle."""
+    import torch
+    W, H, D, w, B = 640, 480, 64, 7, 2
+    sets = [[synthetic_pair(W, H, D, pair_index=90 + 4 * s + i, noise=2)[:2] for i in range(B)] for s in range(3)]
+    eng = ShardedMatcher([0], B, W, H, D, w)
+    frame = W * H
+    try:
+        def fill(pairs):
+            Lp, Rp = eng.input_buffers(0)
+            for i, (l, r) in enumerate(pairs):
+                for ptr, img in ((Lp, l), (Rp, r)):
+                    _copy_to_device(ptr + i * frame, torch.from_numpy(np.ascontiguousarray(img).reshape(-1)).to("cuda:0"))
+
+        hs = []
+        for s in range(3):  # third fill: its slot holds batch 0, still in flight
+            fill(sets[s])
+            h = _submit_resident(eng, B)
+            hs.append(h)
+        for s, h in enumerate(hs):
+            disp = eng.wait(h)[0]
+            for i, (l, r) in enumerate(sets[s]):
+                assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), (s, i)
+    finally:
+        eng.close()
+
+
+def _submit_resident(eng, batch):
+    """usv_batch_sharded_submit on the frames already in input_buffers (L = R = NULL)."""
+    ct = ctypes
+    disp = np.empty((batch, eng.H, eng.W), np.uint8)
+    t = ct.c_longlong()
+    _lib.check("usv_batch_sharded_submit", eng.lib.usv_batch_sharded_submit(
+        eng.handle, None, None, batch, eng.H * eng.W, eng.W, disp.ctypes.data_as(ct.c_void_p), None, None, 0,
+        ct.byref(t)))
+    return {"ticket": t.value, "disp": disp, "dist": None, "keep": ()}

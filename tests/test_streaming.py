@@ -129,3 +129,33 @@ def test_stream_slot_reuse_rules(gpu):
         assert np.array_equal(fs.wait(t), ref)
         fs.release(t)
     fs.close()
+
+
+@pytest.mark.gpu
+def test_stream_views_outlive_the_stream_object(gpu):
+    """Numpy views of the pinned staging keep the stream (and its memory) alive: a view from a temporary
+    FrameStream stays readable after the object is dropped, and close() with a live view defers the free
+    until the view is collected; a closed stream refuses new work."""
+    import gc
+    W, H, D, w = 320, 240, 32, 5
+    L, R, _ = synthetic_pair(W, H, D, pair_index=41)
+    ref = oracle_sad(L, R, D, w, "sad", "sliding")
+
+    def one_frame():
+        fs = FrameStream(W, H, D, w, depth=2)
+        return fs.wait(fs.submit(L, R))  # the FrameStream object itself goes out of scope here
+
+    disp = one_frame()
+    gc.collect()
+    assert np.array_equal(disp, ref)
+    fs = FrameStream(W, H, D, w, depth=2)
+    sl, _ = fs.next_inputs()
+    view = fs.wait(fs.submit(L, R))[10:20]
+    fs.close()  # deferred: sl and view are alive
+    gc.collect()
+    assert np.array_equal(view, ref[10:20]) and sl.shape == (H, W)
+    with pytest.raises(RuntimeError):
+        fs.submit(L, R)
+    del sl, view
+    gc.collect()
+    assert fs._h is None  # the last view went away: the stream was destroyed

@@ -140,7 +140,7 @@ usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
 
 extern "C" {
 
-const char* usv_version(void) { return "usv-mi355x 0.4.0 (gfx950)"; }
+const char* usv_version(void) { return "usv-mi355x 0.4.1 (gfx950, " USV_BUILD_KIND ")"; }
 
 usv_status usv_device_check(int* n_devices) {
     int n = 0;

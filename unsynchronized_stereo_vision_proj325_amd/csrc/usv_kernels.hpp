@@ -5,6 +5,33 @@
 #include <cstddef>
 #include <cstdint>
 
+// Build kind.  The product library (csrc/Makefile) is built with every tuning knob at its default;
+// scripts/build_variant.sh compiles A/B variants with -DUSV_VARIANT_BUILD and knob overrides, and its
+// usv_version() says so ("variant build"), so a variant can never pass for the shipped library
+// (tests/test_capi.py checks the in-tree libusv.so reports "product build").  This header is
+// included before any knob's default is defined, so a knob set on the command line of a product
+// build is an error here.
+#ifndef USV_VARIANT_BUILD
+#if defined(USV_STAMPS) || defined(USV_WGTIME) || defined(USV_PRIO) || defined(USV_SPLIT_CHAIN) ||              \
+    defined(USV_STATIC_RING) || defined(USV_RED_LDS) || defined(USV_RED_PACKED) || defined(USV_FAST_OCC) ||     \
+    defined(USV_L_WHOLE_WORD) || defined(USV_DMA_ONE_M0) || defined(USV_RUN_ADDR) || defined(USV_GEN_WEIGHTS) || \
+    defined(USV_ROUNDS) || defined(USV_MIN_BAND_WINS) || defined(USV_EXTRA_BANDS) || defined(USV_PAIR_PIPE) ||   \
+    defined(USV_NT_DIST) || defined(USV_WIDE_FLUSH) || defined(USV_PAIR_PIPE_R7) || defined(USV_PAIR_SPLIT_R) || \
+    defined(USV_PAIR_PREF) || defined(USV_PAIR_PIECE_OFF) || defined(USV_PAIR_OCC5) || defined(USV_PAIR_OCC7) || \
+    defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) ||                                    \
+    defined(USV_PAIR_GEN_WEIGHTS_NW2) || defined(USV_PAIR_GEN_G_X4) || defined(USV_SSD_FAST) ||                  \
+    defined(USV_SSD_GEN_WEIGHTS) || defined(USV_PAIR) || defined(USV_PAIR_SMALL) || defined(USV_GROUP) ||        \
+    defined(USV_GROUP_OCC) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
+    defined(USV_GROUP_WEIGHTS) || defined(USV_PREP_THREADS) || defined(USV_HSV_PK) || defined(USV_PREP_KU) ||    \
+    defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
+    defined(USV_REMAP_LDS)
+#error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
+#endif
+#define USV_BUILD_KIND "product build"
+#else
+#define USV_BUILD_KIND "variant build"
+#endif
+
 namespace usv {
 
 // Everything a block-match launch needs; one struct so every kernel variant

@@ -30,10 +30,6 @@ namespace {
 #ifndef USV_PREP_THREADS
 #define USV_PREP_THREADS 256  // threads per block of the two frame-prep kernels (512 / 1024 ran slower)
 #endif
-#ifndef USV_PREP_EXP
-#define USV_PREP_EXP 0  // timing experiments only (wrong results): 1 no global bin atomics, 2 no LDS atomics, 3 neither,
-                        // 4 identity LUT, 8 no HSV2BGR, 16 no HSV table build
-#endif
 #ifndef USV_HSV_PK
 #define USV_HSV_PK 0  // 1: the equalize pass's HSV2BGR on packed f32 pairs (hsv2bgr_px2)
 #endif
@@ -186,7 +182,7 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
                 out.c[3 * k] = h;
                 out.c[3 * k + 1] = sat;
                 out.c[3 * k + 2] = val;
-                if (!(USV_PREP_EXP & 2) && k < n) atomicAdd(&lh[wv][val], 1u);
+                if (k < n) atomicAdd(&lh[wv][val], 1u);
             }
             store_px4(hsv, hsv_pitch, y, x, out, v, n);
         });
@@ -195,7 +191,7 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
         uint32_t sum = 0;
 #pragma unroll
         for (int w = 0; w < NWV; ++w) sum += lh[w][t];
-        if (!(USV_PREP_EXP & 1) && sum)
+        if (sum)
             atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blk % kHistCopies) + t], sum);
     }
 }
@@ -307,7 +303,7 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
                     lv = min(max(__float2int_rn(acc * scale), 0), 255);
                 }
             }
-            lut[t] = (USV_PREP_EXP & 4) ? (uint8_t)t : (uint8_t)lv;  // 4: timing experiment (LUT work kept)
+            lut[t] = (uint8_t)lv;
         }
         __syncthreads();
     };
@@ -354,8 +350,7 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
             for (int k = 0; k < 4; ++k) {
                 in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
                 int b, g, r;
-                if (USV_PREP_EXP & 8) b = g = r = in.c[3 * k + 2];  // timing experiment: no HSV2BGR
-                else hsv2bgr_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], b, g, r);
+                hsv2bgr_px(in.c[3 * k], in.c[3 * k + 1], in.c[3 * k + 2], b, g, r);
                 o.c[3 * k] = b;
                 o.c[3 * k + 1] = g;
                 o.c[3 * k + 2] = r;

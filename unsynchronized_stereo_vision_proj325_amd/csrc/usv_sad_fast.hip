@@ -42,12 +42,6 @@ constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_STAMPS
 #define USV_STAMPS 0  // diagnostic build: per-phase s_memtime totals (scripts/stamps.py)
 #endif
-// Timing experiments only (wrong results): USV_EXP=1 no R DMA, 2 no flush
-// barrier, 3 trivial reduction, 4 no L byte extraction,
-// 5 xor/add chain instead of v_sad, 7 no reduction.  Never set in the product build.
-#ifndef USV_EXP
-#define USV_EXP 0
-#endif
 #ifndef USV_PRIO
 // Wave-priority rotation.  The SIMD arbitrates VALU issue by priority, then
 // age: with equal priorities the oldest of the three resident waves runs
@@ -616,16 +610,16 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         const uint8_t* rr = Rdma + row_off(t);
         if constexpr (BUF >= 0) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                ((USV_EXP != 1 ? dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase) : void()), ...);
+                (dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase), ...);
             }(std::make_integer_sequence<int, C::NQ>{});
         } else if constexpr (USV_DMA_ONE_M0 && !C::STATIC_RING) {
             const int buf = t & (NB - 1);
-            if (USV_EXP != 1) dma_row<C::NQ>(rr, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            dma_row<C::NQ>(rr, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
         } else {
             const int buf = t & (NB - 1);
 #pragma unroll
             for (int i = 0; i < C::NQ; ++i)
-                if (USV_EXP != 1) dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
+                dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
         }
     };
 
@@ -659,8 +653,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             int rr = rawR;
             asm volatile("" : "+s"(rr));  // opaque: one row's offset at a time
             const int buf = (t + PD) & (NB - 1);
-            if (USV_EXP != 1)
-                dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
             rawR = rr + a.pitch;
         } else {
             issue_dma(t + PD, std::integral_constant<int, -1>{});
@@ -677,8 +670,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
             for (int j = 0; j < C::NPOS; ++j) {
                 const int bidx = LS::byte(j);
-                if constexpr (USV_EXP == 4) Lv[j] = lw[(bidx >> 2) & 7];  // timing only: no byte extraction
-                else if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
                 else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
@@ -711,13 +703,9 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         Bc[0] = 0;
 #pragma unroll
         for (int j = 0; j < (SP > NB_STEPS ? SP : NB_STEPS); ++j) {
-            if (j < SP) {
-                if constexpr (USV_EXP == 5)  // timing only: same dependency depth, plain adds
-                    A[j + 1] = (A[j] + (Lv[j + HALF] ^ Rv[j + HALF])) + (Lv[j] ^ Rv[j]);
-                else
-                    A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
-                                                          __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
-            }
+            if (j < SP)
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
+                                                      __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
             if (j < NB_STEPS) {
                 const int jj = j + SP;
                 Bc[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[jj + HALF], Rv[jj + HALF],
@@ -767,7 +755,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     if (USV_PRIO) set_prio(prio_phase % 3);
     auto flush = [&](int rows) {
         if (USV_PRIO == 1 || USV_PRIO == 2) set_prio(++prio_phase % 3);
-        if (USV_EXP != 2) lds_barrier();
+        lds_barrier();
         // opaque thread id: the flush's per-lane addresses must not be hoisted
         // out of the row loop (they would stay live through it and spill)
         int tid = threadIdx.x;
@@ -788,7 +776,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     };
     auto emit = [&](const uint32_t(&S)[HALF], int slot) {
         uint32_t m;
-        if constexpr (C::RED_PACKED && USV_EXP == 0) {
+        if constexpr (C::RED_PACKED) {
             m = reduce16_lds_packed(S, tb, lane, rd, dpk, psel);
             comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 2)] = m;
             USV_STAMP(3);
@@ -801,13 +789,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             keys[i] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c050400u);         // (S.lo << 8) | d
             keys[i + HALF] = __builtin_amdgcn_perm(S[i], d_eff, 0x0c070600u);  // (S.hi << 8) | d
         }
-        if constexpr (USV_EXP == 7) {
-            m = keys[lane & 15];  // timing only: no cross-lane reduction at all
-        } else if constexpr (USV_EXP == 3) {
-            m = keys[0];
-#pragma unroll
-            for (int i = 1; i < K; ++i) m ^= keys[i];
-        } else if constexpr (C::RED_LDS) {
+        if constexpr (C::RED_LDS) {
             m = reduce16_lds(keys, tb, lane, rd);
         } else {
             m = reduce16(keys);
@@ -1080,10 +1062,6 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
 #endif
 template <int RAD>
 constexpr bool kPairPipe = USV_PAIR_PIPE && (RAD == 5 || (RAD == 7 && USV_PAIR_PIPE_R7));
-#ifndef USV_PEXP
-#define USV_PEXP 0  // timing experiments (wrong results): 1 no per-row L load, 2 also no L-byte extraction,
-                   // 3 no argmin transpose, 4 no steady-state R DMA, 5 half chain, 6 no ring subtraction
-#endif
 template <int RAD, int NW>
 struct PCfg {
     static constexpr int K = 8;
@@ -1222,11 +1200,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         constexpr int I = decltype(i_tag)::value;
         int t = t_in;
         asm volatile("" : "+s"(t));
-        wait_vmcnt<(PD - 1) * NDMA + (USV_PEXP == 11 ? 4 : 0)>();  // 11: timing experiment (unsafe)
+        wait_vmcnt<(PD - 1) * NDMA>();
         __builtin_amdgcn_wave_barrier();
         if constexpr (WARM) {
             issue_dma(t + PD);
-        } else if constexpr (USV_PEXP == 4) {
         } else {
             int rr = rawR;
             asm volatile("" : "+s"(rr));
@@ -1236,7 +1213,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         }
         // (pipelined argmin: the ring row leaving the window is subtracted first, so its registers
         // are free for this row's staged entries -- no copies)
-        constexpr bool EARLY_SUB = !WARM && kPairPipe<RAD> && USV_PEXP != 6;
+        constexpr bool EARLY_SUB = !WARM && kPairPipe<RAD>;
         if constexpr (EARLY_SUB) {
 #pragma unroll
             for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
@@ -1250,8 +1227,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
             for (int j = 0; j < NPOS; ++j) {
                 const int bidx = LS::byte(j);
-                if (USV_PEXP == 2) Lv[j] = lw[(bidx >> 2) & 7];  // timing experiment: no extraction (wrong)
-                else if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
                 else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
@@ -1280,8 +1256,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
             const uint32_t l = lbyte(j);
-            A[j + 1] = USV_PEXP == 5 ? __builtin_amdgcn_sad_u8(l, E[j + 1], A[j])
-                                     : __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
             pre(jt);
             if constexpr (EARLY_SUB) __builtin_amdgcn_sched_barrier(0);
         };
@@ -1303,15 +1278,13 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
         for (int x = 0; x < K; ++x) {
             const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
-            if constexpr (WARM || EARLY_SUB || USV_PEXP == 6) S[x] = S[x] + h;
+            if constexpr (WARM || EARLY_SUB) S[x] = S[x] + h;
             else S[x] = (S[x] - ring[I][x]) + h;
             ring[I][x] = h;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (WARM) {
             load_lw(t + 1);
-        } else if constexpr (USV_PEXP == 1 || USV_PEXP == 2) {
-            // timing experiment: L row segment loaded once per band (wrong results)
         } else {
             int rl = rawL;
             asm volatile("" : "+s"(rl));
@@ -1329,7 +1302,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     // hold up fewer of the next rows' counted DMA waits.  Needs 4-byte aligned disparity rows.
     const bool wide = USV_WIDE_FLUSH && ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
     auto flush = [&](int rows) {
-        if constexpr (NW > 1 && USV_PEXP != 12) lds_barrier();  // 12: timing experiment, no barrier (racy)
+        if constexpr (NW > 1) lds_barrier();
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
@@ -1350,8 +1323,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 const uint32_t lo = __builtin_amdgcn_perm(k0.y, k0.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k0.w, k0.z, 0x04000c0cu);
                 const uint32_t hi = __builtin_amdgcn_perm(k1.y, k1.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k1.w, k1.z, 0x04000c0cu);
                 const size_t y = (size_t)(y_chunk + tid);
-                if (!(USV_PEXP == 10 && y != 0x7FFFFFFF))
-                    *reinterpret_cast<uint2*>(disp + y * a.disp_pitch + x0) = make_uint2(lo, hi);
+                *reinterpret_cast<uint2*>(disp + y * a.disp_pitch + x0) = make_uint2(lo, hi);
             }
             if (dist && tid < 4 * rows) {
                 struct __attribute__((aligned(8))) D2 { double a, b; };
@@ -1363,8 +1335,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                     kk = make_uint2(min(kk.x, m.x), min(kk.y, m.y));
                 }
                 const size_t y = (size_t)(y_chunk + r);
-                if (!(USV_PEXP == 10 && y != 0x7FFFFFFF))
-                    if constexpr (USV_NT_DIST) {  // experiment: write-once map as non-temporal stores
+                if constexpr (USV_NT_DIST) {  // experiment: write-once map as non-temporal stores
                         typedef double v2d __attribute__((ext_vector_type(2)));
                         v2d v = {lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
                         __builtin_nontemporal_store(v, reinterpret_cast<v2d*>(dist + y * a.dist_pitch + x0 + 2 * q));
@@ -1384,7 +1355,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
             const uint32_t dv = key & 0xFFu;
             const size_t y = (size_t)(y_chunk + row);
-            if (USV_PEXP == 10 && y != 0x7FFFFFFF) continue;  // timing experiment: no output stores (wrong)
             disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
             if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
         }
@@ -1399,11 +1369,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     //              lanes of the pixel, one comb word per pixel.
     uint4 trq[2];
     auto tr_issue = [&](const uint32_t(&S)[K]) {
-        if constexpr (USV_PEXP == 7) {  // timing experiment: no LDS transpose (wrong results)
-            trq[0] = make_uint4(S[0], S[1], S[2], S[3]);
-            trq[1] = make_uint4(S[4], S[5], S[6], S[7]);
-            return;
-        }
 #pragma unroll
         for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
         asm volatile("" ::: "memory");
@@ -1419,11 +1384,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     uint32_t fv[16], fb[5], fm;
     auto tr_piece = [&](auto jt, int slot) {
         constexpr int J = decltype(jt)::value;
-        if constexpr (USV_PEXP == 8) {  // timing experiment: transpose kept, key / min VALU skipped (wrong)
-            if constexpr (J == 15)
-                comb[((cb * KRB + slot) * NW + wave) * K + (lane >> 3)] =
-                    trq[0].x ^ trq[0].y ^ trq[0].z ^ trq[0].w ^ trq[1].x ^ trq[1].y ^ trq[1].z ^ trq[1].w;
-        } else if constexpr (J < 8) {
+        if constexpr (J < 8) {
             constexpr int j = J >> 2, e = J & 3;
             const uint32_t w = e == 0 ? trq[j].x : e == 1 ? trq[j].y : e == 2 ? trq[j].z : trq[j].w;
             // (r = 7: the second window's d table and both d + 1 tables are rebuilt per row from
@@ -1435,19 +1396,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             }
             fv[8 * j + 2 * e] = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
             fv[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
-        } else if constexpr (USV_PEXP == 9 && J >= 8 && J <= 11) {  // experiment: two-operand min tree
-            if constexpr (J == 8) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) fv[i] = min(fv[i], fv[i + 8]);
-            } else if constexpr (J == 9) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) fv[i] = min(fv[i], fv[i + 4]);
-            } else if constexpr (J == 10) {
-                fv[0] = min(fv[0], fv[2]);
-                fv[1] = min(fv[1], fv[3]);
-            } else {
-                fm = min(fv[0], fv[1]);
-            }
         } else if constexpr (J == 8) {
             fb[0] = min(min(fv[0], fv[1]), fv[2]);
             fb[1] = min(min(fv[3], fv[4]), fv[5]);
@@ -1675,376 +1623,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     wait_vmcnt<0>();
 }
 
-// ===================================================================================
-// Paired kernel with K = 16 output columns per lane (w = 11, even 64 < D <= 128; one wave per
-// workgroup, TWO waves per SIMD).
-//
-// The same lane = (d, d + 1) mapping as the K = 8 kernel above, twice the columns: per (pixel,
-// disparity) the prefix chain takes (16 + 11) / 16 = 1.69 v_sad instead of (8 + 11) / 8 = 2.38, and
-// the per-row fixed costs (L-byte extraction, row addressing, the three R DMAs, waits) are spread
-// over 2048 candidates instead of 1024.  The 11-row H ring doubles to 176 VGPRs, which two waves per
-// SIMD (256 VGPRs each) hold; the round-2 occupancy A/B found 2 and 3 waves per SIMD equally fast
-// for the K = 8 kernel (profiles/probes_r02/ab_pair_ablations_r02.txt, occ2).
-//   * H is formed as soon as the chain has passed a column's right edge (H[x] = A[x + 11] - A[x])
-//     and folded into S at once, so only ~12 prefix values are live, and the row's staged entries
-//     are read in two batches.
-//   * Argmin: lane l stores its 16 packed words (pixel-major rows of 64 lanes); lane m = 4p + q
-//     reads the 16 words of pixel p from lanes 16q .. 16q + 15 as four 16-B windows, visited in
-//     the rotated order (j + p) & 3; each word gives two keys (cost << 8) | d by v_perm, folded
-//     into one accumulator with v_min3; two quad DPP rounds finish.  The 18 pieces ride on the
-//     next row's chain steps (pipelined as in the K = 8 r = 5 kernel).
-template <int RAD, int KK>
-struct P16Cfg {
-    static constexpr int K = KK;
-    static constexpr int KS = 16;                       // comb slots per row (pixel slots of the transpose)
-    static constexpr int WIN = 2 * RAD + 1;
-    static constexpr int NPOS = K + 2 * RAD;            // chain steps
-    static constexpr int NE = NPOS + 1;                 // staged entries a lane reads per row
-    static constexpr int VEC = 2;
-    static constexpr int NE_V = (NE + VEC - 1) / VEC * VEC;
-    static constexpr int NR = 2 * 63 + NE_V;            // entries a wave stages per row
-    static constexpr int NQ = (NR + 63) / 64;           // DMA instructions per row
-    static constexpr int NRS = NQ * 64;
-    static constexpr int NB = 8;
-    static constexpr int PD = NB - 1;
-    static constexpr int KRB = WIN;
-    static constexpr int RBUF_OFF = 0;
-    static constexpr int TB_OFF = RBUF_OFF + NB * NRS;
-    static constexpr int TB_WORDS = K * 64;
-    static constexpr int COMB_OFF = TB_OFF + TB_WORDS;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * KS;
-    static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
-    static_assert(RAD == 5, "K = 12 / 16 paired kernel: w = 11");
-    static_assert(K == 12 || K == 16, "12 or 16 columns per lane");
-    static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
-    static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
-};
-#ifndef USV_P16_PIECE_OFF
-#define USV_P16_PIECE_OFF 4  // chain step of the first argmin piece
-#endif
-#ifndef USV_P16_EBATCH
-#define USV_P16_EBATCH 4  // vector reads (2 entries each) in the first batch of a row's staged entries
-#endif
-
-template <int RAD, int KK, int EDGE>
-__device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
-                                                 uint8_t* __restrict__ disp, double* __restrict__ dist,
-                                                 const MatchArgs& a, uint32_t* smem, int lane, int x0, int y_begin,
-                                                 int y_end) {
-    using C = P16Cfg<RAD, KK>;
-    using LS = LSeg<RAD, EDGE, C::K>;
-    // (K = 12 interior tiles need 7 dwords: load 8, still inside the row since x0 <= W - 2K)
-    constexpr int NLD = LS::NLD == 7 ? 8 : LS::NLD;
-    using LWords = typename SWords<NLD>::T;
-    constexpr int WIN = C::WIN, K = C::K, KS = C::KS, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
-    constexpr int NDMA = C::NQ;
-    const int lmax = min(63, a.D / 2 - 1);
-    const int l_eff = min(lane, lmax);
-    const int cbase = x0 - RAD - (2 * 63 + 1);  // first R column staged
-    uint32_t* rbuf = smem + C::RBUF_OFF;
-    uint32_t* comb = smem + C::COMB_OFF;
-    uint32_t* tb = smem + C::TB_OFF;
-    // transposed reads: lane m = 4p + q reads windows (j + p) & 3 of words 64 p + 16 q .. + 15
-    const int tp = lane >> 2, tq = lane & 3;
-    const uint32_t rd0 = (uint32_t)(16 * tp + 4 * tq);  // uint4 index of window 0
-    // d bytes of window w: source lane 16 q + 4 w + e -> d = 2 (16 q + 4 w + e) (max 126; lanes past
-    // lmax replay lmax's data with a larger d, so their keys never win)
-    const uint32_t dbase = (uint32_t)(32 * tq) * 0x01010101u + 0x06040200u;  // + w * 0x08080808 for window w
-    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
-    const int s_l = 2 * (63 - l_eff);
-    const int nout = y_end - y_begin;
-    const int T = nout + 2 * RAD;
-    const int Hm1 = a.H - 1, Wm1 = a.W - 1;
-    auto row_off = [&](int t) -> uint32_t {
-        const int y = min(max(y_begin - RAD + t, 0), Hm1);
-        return (uint32_t)(y * a.pitch);
-    };
-    const uint8_t* const Lseg = L + LS::base(x0);
-    const uint8_t* const Rdma = R - kDmaBias;
-    const int y0 = y_begin - RAD;
-    const int last_off = Hm1 * a.pitch;
-    int rawL = (y0 + WIN + 1) * a.pitch, rawR = (y0 + WIN + PD) * a.pitch;
-    const su4 rsrc = [&] {
-        const uint64_t base = reinterpret_cast<uint64_t>(Rdma);
-        su4 r;
-        r[0] = (uint32_t)base;
-        r[1] = (uint32_t)(base >> 32);
-        r[2] = 0xFFFFFFFFu;
-        r[3] = 0x00020000u;
-        return r;
-    }();
-    uint32_t colRb[C::NQ];
-#pragma unroll
-    for (int i = 0; i < C::NQ; ++i)
-        colRb[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1) + kDmaBias - 256u * (uint32_t)i;
-    const uint32_t rbase = lds_addr(rbuf);
-    auto issue_dma = [&](int t) {
-        const int buf = t & (NB - 1);
-        dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
-    };
-    LWords lw_next;
-    auto load_lw = [&](int t) { lw_next = s_load_words_pin<NLD>(Lseg, row_off(t)); };
-    using VT = typename VecT<C::VEC>::T;
-    constexpr int NV = C::NE_V / C::VEC;
-    constexpr int NV1 = USV_P16_EBATCH < NV ? USV_P16_EBATCH : NV;
-    constexpr int OFF = USV_P16_PIECE_OFF;
-
-    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
-        constexpr bool WARM = decltype(warm_tag)::value;
-        constexpr int I = decltype(i_tag)::value;
-        int t = t_in;
-        asm volatile("" : "+s"(t));
-        wait_vmcnt<(PD - 1) * NDMA>();
-        __builtin_amdgcn_wave_barrier();
-        if constexpr (WARM) {
-            issue_dma(t + PD);
-        } else {
-            int rr = rawR;
-            asm volatile("" : "+s"(rr));
-            const int buf = (t + PD) & (NB - 1);
-            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
-            rawR = rr + a.pitch;
-        }
-        if constexpr (!WARM) {
-#pragma unroll
-            for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
-        }
-        uint32_t Lv[NPOS];
-        {
-            wait_lgkm0_pin<NLD>(lw_next);
-            LWords cur = lw_next;
-            uint32_t lw[8];
-            unpack_words<NLD>(cur, lw);
-#pragma unroll
-            for (int j = 0; j < NPOS; ++j) {
-                const int bidx = LS::byte(j);
-                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
-                else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
-            }
-        }
-        int boff = (t & (NB - 1)) * C::NRS;
-        asm volatile("" : "+s"(boff));
-        const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
-        uint32_t E[C::NE_V];
-        auto read_e = [&](int k0, int k1) {
-#pragma unroll
-            for (int k = k0; k < k1; ++k) {
-                const VT v = rb[k];
-#pragma unroll
-                for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
-            }
-        };
-        read_e(0, NV1);
-        uint32_t A[NPOS + 1];
-        A[0] = 0;
-        auto chain_step = [&](auto jt) {
-            constexpr int j = decltype(jt)::value;
-            // later entries in batches of two vector reads, issued EB steps before their first use
-            constexpr int EB = 4;
-            if constexpr (j % 4 == 0 && (j + EB) / 2 >= NV1 && (j + EB) / 2 < NV) {
-                constexpr int k0 = (j + EB) / 2 > NV1 ? (j + EB) / 2 : NV1;
-                constexpr int k1 = (j + EB) / 2 + 2 < NV ? (j + EB) / 2 + 2 : NV;
-                asm volatile("" ::: "memory");
-                read_e(k0, k1);
-            }
-            const uint32_t l = Lv[j];
-            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
-            if constexpr (j + 1 >= WIN) {  // column x = j + 1 - WIN is complete: fold its H at once
-                constexpr int x = j + 1 - WIN;
-                const uint32_t h = A[j + 1] - A[x];  // both halves in [0, 65535], no borrow
-                S[x] = S[x] + h;
-                ring[I][x] = h;
-            }
-            if constexpr (j >= OFF) pre(std::integral_constant<int, j - OFF>{});
-            if constexpr (!WARM) __builtin_amdgcn_sched_barrier(0);
-        };
-        [&]<int... J>(std::integer_sequence<int, J...>) {
-            (chain_step(std::integral_constant<int, J>{}), ...);
-        }(std::make_integer_sequence<int, NPOS>{});
-        [&]<int... J>(std::integer_sequence<int, J...>) {  // pieces that did not fit on the chain
-            ((J + OFF >= NPOS ? pre(std::integral_constant<int, J>{}) : void()), ...);
-        }(std::make_integer_sequence<int, 18>{});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (WARM) {
-            load_lw(t + 1);
-        } else {
-            int rl = rawL;
-            asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_pin<NLD>(Lseg, (uint32_t)min(rl, last_off));
-            rawL = rl + a.pitch;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    int cb = 0, y_chunk = y_begin;
-    const bool wide = ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
-    auto flush = [&](int rows) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const uint32_t* crow = comb + (cb * KRB) * KS;
-        if (wide) {
-            if (tid < rows) {  // lane r: row r's K disparity bytes (byte 0 of each key), one store
-                const uint4* kr = reinterpret_cast<const uint4*>(crow + tid * KS);
-                uint32_t o[K / 4];
-#pragma unroll
-                for (int i = 0; i < K / 4; ++i) {
-                    const uint4 k = kr[i];
-                    o[i] = __builtin_amdgcn_perm(k.y, k.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k.w, k.z, 0x04000c0cu);
-                    asm volatile("" ::: "memory");  // one 16-B window live at a time
-                }
-                uint8_t* dp = disp + (size_t)(y_chunk + tid) * a.disp_pitch + x0;
-                if constexpr (K == 16) *reinterpret_cast<uint4*>(dp) = make_uint4(o[0], o[1], o[2], o[3]);
-                else *reinterpret_cast<uint3*>(dp) = make_uint3(o[0], o[1], o[2]);
-            }
-            if (dist && tid < (K / 4) * rows) {  // lane (K/4) r + q: distances 4q .. 4q + 3 of row r
-                struct __attribute__((aligned(8))) D2 { double a, b; };
-                const int r = tid / (K / 4), q = tid - r * (K / 4);
-                const uint4 k = reinterpret_cast<const uint4*>(crow + r * KS)[q];
-                double* o = dist + (size_t)(y_chunk + r) * a.dist_pitch + x0 + 4 * q;
-                reinterpret_cast<D2*>(o)[0] = D2{lut_s[k.x & 0xFFu], lut_s[k.y & 0xFFu]};
-                reinterpret_cast<D2*>(o)[1] = D2{lut_s[k.z & 0xFFu], lut_s[k.w & 0xFFu]};
-            }
-        } else {
-            for (int i = tid; i < rows * K; i += 64) {
-                const int row = i / K, px = i - row * K;
-                const uint32_t dv = crow[row * KS + px] & 0xFFu;
-                const size_t y = (size_t)(y_chunk + row);
-                disp[y * a.disp_pitch + x0 + px] = (uint8_t)dv;
-                if (dist) dist[y * a.dist_pitch + x0 + px] = lut_s[dv];
-            }
-        }
-        y_chunk += rows;
-        cb ^= 1;
-    };
-    uint4 trq[4];
-    auto tr_issue = [&](const uint32_t(&S)[K]) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
-        asm volatile("" ::: "memory");
-        trq[0] = reinterpret_cast<const uint4*>(tb)[rd0 + (uint32_t)(tp & 3)];
-        asm volatile("" ::: "memory");
-    };
-    uint32_t acc = 0, dh = 0, dl = 0;
-    auto tr_piece = [&](auto jt, int slot) {
-        constexpr int J = decltype(jt)::value;
-        // window w is read at piece 4 w - 3 (w >= 1), a few pieces before its first key: one 16-B
-        // window live at a time keeps the K = 16 kernel inside 256 VGPRs
-        if constexpr (J < 16 && (J & 3) == 1 && J < 13) {
-            constexpr int w = (J >> 2) + 1;
-            asm volatile("" ::: "memory");
-            trq[w] = reinterpret_cast<const uint4*>(tb)[rd0 + (uint32_t)((w + tp) & 3)];
-            asm volatile("" ::: "memory");
-        }
-        if constexpr (J < 16) {
-            constexpr int jw = J >> 2, e = J & 3;
-            const uint32_t w = e == 0 ? trq[jw].x : e == 1 ? trq[jw].y : e == 2 ? trq[jw].z : trq[jw].w;
-            if constexpr (e == 0) {
-                dl = dbase + (uint32_t)((jw + tp) & 3) * 0x08080808u;
-                dh = dl + 0x01010101u;
-            }
-            const uint32_t klo = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
-            const uint32_t khi = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
-            acc = J == 0 ? min(klo, khi) : min(min(acc, klo), khi);
-        } else if constexpr (J == 16) {
-            acc = min(acc, dpp<kQuadSwap1>(acc));
-        } else if constexpr (J == 17) {
-            acc = min(acc, dpp<kQuadSwap2>(acc));
-            comb[(cb * KRB + slot) * KS + tp] = acc;  // pixel slots >= K (K = 12) are padding
-        }
-    };
-    auto tr_finish = [&](int slot) {
-        [&]<int... J>(std::integer_sequence<int, J...>) {
-            (tr_piece(std::integral_constant<int, J>{}, slot), ...);
-        }(std::make_integer_sequence<int, 18>{});
-    };
-    auto no_pre = [](auto) {};
-
-    uint32_t S[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) S[i] = 0;
-    uint32_t ring[WIN][K];
-    static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
-    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
-    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
-    load_lw(0);
-    using WarmT = std::integral_constant<bool, true>;
-    using SteadyT = std::integral_constant<bool, false>;
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring, no_pre), ...);
-    }(std::make_integer_sequence<int, WIN>{});
-    tr_issue(S);
-    __builtin_amdgcn_sched_barrier(0);
-    static_assert(KRB == WIN, "pending slot = row index in the unrolled group");
-    auto step = [&](int t0, auto i_tag) {
-        constexpr int I = decltype(i_tag)::value;
-        do_row(t0 + I, SteadyT{}, i_tag, S, ring, [&](auto jt) { tr_piece(jt, I); });
-        if constexpr (I == KRB - 1) flush(KRB);
-        tr_issue(S);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    for (int t0 = WIN; t0 < T; t0 += WIN) {
-        [&]<int... I>(std::integer_sequence<int, I...>) {
-            bool go = true;
-            ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
-        }(std::make_integer_sequence<int, WIN>{});
-    }
-    wait_lgkm0_pin<NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
-    {
-        const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
-        tr_finish(last);
-        if (last == KRB - 1) flush(KRB);
-    }
-    const int rest = nout % KRB;
-    if (rest) flush(rest);
-    wait_vmcnt<0>();
-}
-
-#ifndef USV_P16_OCC
-#define USV_P16_OCC 2  // waves per SIMD the K = 16 paired kernel is compiled for
-#endif
-template <int RAD, int KK>
-__global__ __launch_bounds__(64, USV_P16_OCC) void sad_pair16_kernel(const uint8_t* __restrict__ L,
-                                                                     const uint8_t* __restrict__ R,
-                                                                     uint8_t* __restrict__ disp,
-                                                                     double* __restrict__ dist, MatchArgs a,
-                                                                     BandPlan P) {
-    using C = P16Cfg<RAD, KK>;
-    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
-    const int lane = threadIdx.x & 63;
-    const unsigned total = gridDim.x, lin = blockIdx.x;
-    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
-    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
-    const bool past = tile >= per_pair && P.extra > 0;
-    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
-    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
-    const unsigned pair = past ? 0u : tile / per_pair;
-    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
-    const unsigned long_run = base + 1u, split = rem * long_run;
-    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
-                                  (unsigned)P.gen_g, P.weights);
-    const unsigned pre = bs.pre, tot = bs.tot;
-    const int xt = (int)col_xt;
-    const int n_xt = P.n_xt;
-    int x0 = xt * C::K;
-    if (xt == n_xt - 1) x0 = a.W - C::K;
-    else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
-    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
-    L += (size_t)pair * a.pair_stride;
-    R += (size_t)pair * a.pair_stride;
-    disp += (size_t)pair * a.disp_stride;
-    if (dist) dist += (size_t)pair * a.dist_stride;  // (the table is staged inside the band loop)
-    if (y_end <= y_begin) return;
-    if (xt == 0)
-        pair16_band_loop<RAD, KK, kLeft>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
-    else if (xt == n_xt - 1)
-        pair16_band_loop<RAD, KK, kRight>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
-    else
-        pair16_band_loop<RAD, KK, kInterior>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
-}
-
 #ifndef USV_PAIR_OCC7
 #define USV_PAIR_OCC7 3  // waves per SIMD the r = 7 paired kernel is compiled for
 #endif
@@ -2158,45 +1736,6 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
               : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
-    return hipGetLastError();
-}
-
-template <int RAD, int KK>
-int resident_p16_blocks_per_cu() {
-    static const int n = [] {
-        int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair16_kernel<RAD, KK>, 64, 0) != hipSuccess || v <= 0)
-            v = 1;
-        return v;
-    }();
-    return n;
-}
-
-template <int RAD, int KK>
-hipError_t launch_pair16_r(const MatchArgs& a, hipStream_t s) {
-    constexpr int K = P16Cfg<RAD, KK>::K, WIN = 2 * RAD + 1;
-    BandPlan P{};
-    P.n_xt = (a.W + K - 1) / K;
-    const int per_cu = resident_p16_blocks_per_cu<RAD, KK>();
-    const long slots = (long)cu_count() * per_cu;
-    const long NC = (long)P.n_xt * a.batch;
-    long m = slots / NC;
-    if (m < 1) m = 1;
-    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
-    if (m > m_max) m = m_max;
-    P.m = (int)m;
-    const long ex = slots - NC * m;
-    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && ex > 0 && ex < P.n_xt &&
-               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
-    const long total = NC * m + P.extra;
-    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
-    P.gen_g = (int)(4L * (cu_count() / 8));
-    if (P.gen_g < 1) P.gen_g = 1;
-#ifndef USV_P16_WEIGHTS
-#define USV_P16_WEIGHTS 0x01010101u  // band heights by dispatch generation (equal: not fitted yet)
-#endif
-    P.weights = per_cu == 8 && total > 2L * 8 * P.gen_g ? USV_P16_WEIGHTS : 0x01010101u;
-    hipLaunchKernelGGL((sad_pair16_kernel<RAD, KK>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a, P);
     return hipGetLastError();
 }
 
@@ -2626,9 +2165,6 @@ hipError_t launch_ssd_r(const MatchArgs& a, hipStream_t s) {
     return launch_ssd_rn<RAD, 4>(a, s);
 }
 
-#ifndef USV_PAIR16
-#define USV_PAIR16 0  // 12 or 16:the wide paired kernel with that many columns per lane (w = 11, even 64 < D <= 128); 0 = off
-#endif
 #ifndef USV_PAIR
 #define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
 #endif
@@ -2690,16 +2226,8 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
             default: return hipErrorInvalidValue;
         }
     }
-#ifdef USV_DEV_ONLY_RAD  // development: build a single instantiation for ISA inspection
-    return launch_rn<USV_DEV_ONLY_RAD, USV_DEV_ONLY_NW>(a, s);
-#elif defined(USV_EXP_PAIR_ONLY)  // timing experiments: the paired kernel only (configs C and E)
-    if (!pair_path_supported(a)) return hipErrorInvalidValue;
-    if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
-    return a.w == 11 ? launch_pair_r<5>(a, s) : a.w == 15 ? launch_pair_r<7>(a, s) : hipErrorInvalidValue;
-#else
     if (group_path_supported(a)) return launch_group(a, s);  // usv_sad_group.hip: D <= 64, w <= 9
     if (pair_path_supported(a)) {
-        if (USV_PAIR16 && a.w == 11 && a.D <= 128) return launch_pair16_r<5, USV_PAIR16 ? USV_PAIR16 : 16>(a, s);
         switch ((a.w - 1) / 2) {
 #if USV_PAIR_SMALL
             case 2: return launch_pair_r<2>(a, s);
@@ -2722,7 +2250,6 @@ hipError_t launch_fast(const MatchArgs& a, hipStream_t s) {
         case 7: return launch_r<7>(a, s);
         default: return hipErrorInvalidValue;
     }
-#endif
 }
 
 }  // namespace usv

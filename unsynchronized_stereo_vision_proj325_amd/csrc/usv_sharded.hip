@@ -49,6 +49,7 @@ struct usv_sharded_engine {
         double* dist = nullptr;           // devices[0]: max_pairs * frame doubles (lazy)
         uint8_t* hdisp = nullptr;         // pinned host copy of `gathered` (lazy)
         hipEvent_t done = nullptr;        // on devices[0]'s stream after the last step
+        std::vector<hipEvent_t> h2d;      // per device: after its host-input copies (pageable sources)
         long long ticket = -1;            // batch in flight here, -1 = free
         int batch = 0;
         uint8_t* out_disp = nullptr;      // the caller's host outputs of that batch
@@ -58,6 +59,13 @@ struct usv_sharded_engine {
     Slot slot[kSlots];
     long long next = 0;   // ticket of the next submit
     int last_done = -1;   // slot of the last completed batch (usv_sharded_outputs)
+    // Batches completed implicitly (a submit or usv_sharded_input_buffers needed their slot) and not
+    // waited for yet: usv_batch_sharded_wait(ticket) reports each one's own completion status.
+    struct Retired {
+        long long ticket;
+        usv_status status;
+    };
+    std::vector<Retired> retired;
 };
 
 namespace {
@@ -83,6 +91,7 @@ void release(usv_sharded_engine* e) {
             if (k < (int)s.L.size()) (void)hipFree(s.L[k]);
             if (k < (int)s.R.size()) (void)hipFree(s.R[k]);
             if (k > 0 && k < (int)s.disp.size()) (void)hipFree(s.disp[k]);
+            if (k < (int)s.h2d.size() && s.h2d[k]) (void)hipEventDestroy(s.h2d[k]);
             if (k == 0) {
                 (void)hipFree(s.gathered);
                 (void)hipFree(s.dist);
@@ -106,14 +115,21 @@ usv_status drain(usv_sharded_engine* e, usv_sharded_engine::Slot& s) {
 
 usv_status complete(usv_sharded_engine* e, int si);
 
+// Complete slot si's batch because its slot is needed again; its status is kept for the wait on its
+// ticket (so a caller can tell a delivered batch from a failed one) instead of being reported by the
+// call that needed the slot.  The record holds the last 64 such batches.
+void complete_implicit(usv_sharded_engine* e, int si) {
+    const long long t = e->slot[si].ticket;
+    const usv_status st = complete(e, si);
+    if (e->retired.size() >= 64) e->retired.erase(e->retired.begin());
+    e->retired.push_back({t, st});
+}
+
 usv_status submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int batch, size_t pair_stride, int pitch,
                   uint8_t* disp, double* dist_cm, const double* lut_cm, bool want_dist, long long* ticket) {
     const int si = (int)(e->next % kSlots);
     usv_sharded_engine::Slot& s = e->slot[si];
-    if (s.ticket >= 0) {  // both slots busy: finish the older batch first
-        const usv_status st = complete(e, si);
-        if (st != USV_OK) return st;
-    }
+    if (s.ticket >= 0) complete_implicit(e, si);  // both slots busy: finish the older batch first
     const bool host_in = L || R;
     const size_t frame = e->frame;
     const size_t shard_bytes = (size_t)e->per * frame;
@@ -138,9 +154,16 @@ usv_status submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int
                     return;
                 }
             }
+            if (hipEventRecord(s.h2d[k], hs) != hipSuccess) {
+                st[k] = USV_ERR_HIP;
+                return;
+            }
         }
         st[k] = usv_sad_disparity_batch(s.L[k], s.R[k], count, frame, e->W, e->H, e->W, e->D, e->w, e->metric,
                                         s.disp[k], frame, e->W, nullptr, 0, 0, nullptr, hs);
+        // The host inputs may be pageable, where an async copy need not have read its source when the
+        // call returns: wait for the copies (not the kernel) so the caller may reuse L / R at once.
+        if (host_in && hipEventSynchronize(s.h2d[k]) != hipSuccess && st[k] == USV_OK) st[k] = USV_ERR_HIP;
     };
     if (e->n == 1) {
         work(0);
@@ -291,6 +314,7 @@ usv_status usv_sharded_create(const int* devices, int n_devices, int max_pairs, 
         s.L.assign(n_devices, nullptr);
         s.R.assign(n_devices, nullptr);
         s.disp.assign(n_devices, nullptr);
+        s.h2d.assign(n_devices, nullptr);
     }
     for (int k = 0; k < n_devices; ++k) {
         if (hipSetDevice(devices[k]) != hipSuccess) {
@@ -299,6 +323,7 @@ usv_status usv_sharded_create(const int* devices, int n_devices, int max_pairs, 
         }
         for (auto& s : e->slot) {
             if (hipStreamCreateWithFlags(&s.stream[k], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&s.h2d[k], hipEventDisableTiming) != hipSuccess ||
                 hipMalloc(&s.L[k], shard_bytes) != hipSuccess || hipMalloc(&s.R[k], shard_bytes) != hipSuccess) {
                 release(e);
                 return USV_ERR_HIP;
@@ -335,7 +360,14 @@ usv_status usv_sharded_destroy(usv_sharded_engine* e) {
 
 usv_status usv_sharded_input_buffers(usv_sharded_engine* e, int k, uint8_t** L, uint8_t** R) {
     if (!e || k < 0 || k >= e->n || !L || !R) return USV_ERR_INVALID_ARG;
-    const auto& s = e->slot[e->next % kSlots];  // the slot the next submit uses
+    const int si = (int)(e->next % kSlots);  // the slot the next submit uses
+    if (e->slot[si].ticket >= 0) {
+        // that slot's batch may still be reading these buffers: complete it first (its status stays
+        // with its ticket), so filling them cannot race with the running batch
+        DeviceRestore restore;
+        complete_implicit(e, si);
+    }
+    const auto& s = e->slot[si];
     *L = s.L[k];
     *R = s.R[k];
     return USV_OK;
@@ -365,7 +397,16 @@ usv_status usv_batch_sharded_submit(usv_sharded_engine* e, const uint8_t* L, con
 usv_status usv_batch_sharded_wait(usv_sharded_engine* e, long long ticket) {
     if (!e || ticket < 0) return USV_ERR_INVALID_ARG;
     const int si = (int)(ticket % kSlots);
-    if (e->slot[si].ticket != ticket) return USV_ERR_INVALID_ARG;
+    if (e->slot[si].ticket != ticket) {
+        // completed implicitly when its slot was needed: report that completion's status once
+        for (auto it = e->retired.begin(); it != e->retired.end(); ++it)
+            if (it->ticket == ticket) {
+                const usv_status st = it->status;
+                e->retired.erase(it);
+                return st;
+            }
+        return USV_ERR_INVALID_ARG;
+    }
     DeviceRestore restore;
     return complete(e, si);
 }

@@ -163,8 +163,10 @@ usv_status usv_frame_stream_submit(usv_frame_stream* e, const uint8_t* L, const 
     stage(L, s.hL);
     stage(R, s.hR);
     if (hipMemcpyAsync(s.dL, s.hL, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
-        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess)
+        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+        (void)hipStreamSynchronize(s.stream);  // a first copy that was enqueued may still read the staging
         return USV_ERR_HIP;
+    }
     const bool dd = e->flags & USV_STREAM_DEVICE_DIST;
     usv_status st = usv_sad_disparity_ex(s.dL, s.dR, e->W, e->H, e->W, e->D, e->w, e->metric, s.dDisp, e->W,
                                          dd ? s.dDist : nullptr, e->W, dd ? e->lut : nullptr, USV_KERNEL_AUTO,

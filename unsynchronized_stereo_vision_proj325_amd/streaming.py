@@ -18,6 +18,7 @@ asked, or computed on the device with ``device_distance=True``.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 
@@ -27,10 +28,22 @@ from .engine import distance_lut_cm
 _METRICS = {"sad": _lib.METRIC_SAD, "ssd": _lib.METRIC_SSD}
 
 
-def _view(ptr: int, shape, dtype) -> np.ndarray:
-    n = int(np.prod(shape)) * np.dtype(dtype).itemsize
-    buf = (ctypes.c_uint8 * n).from_address(ptr)
-    return np.frombuffer(buf, dtype=dtype).reshape(shape)
+class _PinnedView:
+    """Array interface over a FrameStream's pinned memory that holds a reference to the stream: a numpy
+    view's base is this object, so while any view (or a slice of one) is alive the stream -- and the
+    pinned allocation behind it -- cannot be collected, and an explicit close() defers the free until
+    the last view is gone (FrameStream._views)."""
+
+    def __init__(self, owner, ptr: int, shape, dtype):
+        self._owner = owner
+        self.__array_interface__ = {"data": (ptr, False), "shape": tuple(shape), "typestr": np.dtype(dtype).str,
+                                    "version": 3}
+
+
+def _view(owner, ptr: int, shape, dtype) -> np.ndarray:
+    holder = _PinnedView(owner, ptr, shape, dtype)
+    owner._views.add(holder)
+    return np.asarray(holder)
 
 
 class FrameStream:
@@ -39,6 +52,8 @@ class FrameStream:
     def __init__(self, W: int, H: int, D: int = 128, w: int = 11, metric: str = "sad", depth: int = 3,
                  device_distance: bool = False):
         self._lib = _lib.load()
+        self._views = weakref.WeakSet()  # live _PinnedView holders (numpy views of the pinned staging)
+        self._closing = False
         self.W, self.H, self.D, self.w = W, H, D, w
         self.device_distance = device_distance
         h = ctypes.c_void_p()
@@ -48,9 +63,26 @@ class FrameStream:
         self._h = h
 
     def close(self) -> None:
-        if self._h:
-            _lib.check("usv_frame_stream_destroy", self._lib.usv_frame_stream_destroy(self._h))
-            self._h = None
+        """Destroy the stream (its pinned host memory included).  While numpy views returned by
+        next_inputs() / wait() are still alive the free is deferred until the last one is collected,
+        so a view can never point at released memory; the stream takes no new submits meanwhile."""
+        self._closing = True
+        if not self._h:
+            return
+        live = list(self._views)
+        if live:
+            for holder in live:
+                weakref.finalize(holder, self._destroy_if_unviewed)
+            return
+        self._destroy()
+
+    def _destroy_if_unviewed(self) -> None:
+        if self._h and not len(self._views):
+            self._destroy()
+
+    def _destroy(self) -> None:
+        h, self._h = self._h, None
+        _lib.check("usv_frame_stream_destroy", self._lib.usv_frame_stream_destroy(h))
 
     def __del__(self):
         try:
@@ -58,15 +90,21 @@ class FrameStream:
         except Exception:
             pass
 
+    def _require_open(self) -> None:
+        if self._closing or not self._h:
+            raise RuntimeError("FrameStream is closed")
+
     def next_inputs(self) -> tuple[np.ndarray, np.ndarray]:
         """Pinned (H, W) u8 staging of the next submit's slot (write the frames there)."""
+        self._require_open()
         lp, rp = ctypes.c_void_p(), ctypes.c_void_p()
         _lib.check("usv_frame_stream_next_inputs",
                    self._lib.usv_frame_stream_next_inputs(self._h, ctypes.byref(lp), ctypes.byref(rp)))
-        return _view(lp.value, (self.H, self.W), np.uint8), _view(rp.value, (self.H, self.W), np.uint8)
+        return _view(self, lp.value, (self.H, self.W), np.uint8), _view(self, rp.value, (self.H, self.W), np.uint8)
 
     def submit(self, L: np.ndarray, R: np.ndarray) -> int:
         """Enqueue one host pair ((H, W) u8, unit column stride); returns the frame's ticket."""
+        self._require_open()
         for a, n in ((L, "L"), (R, "R")):
             if not isinstance(a, np.ndarray) or a.dtype != np.uint8 or a.shape != (self.H, self.W) or \
                     a.strides[1] != 1:
@@ -82,16 +120,18 @@ class FrameStream:
     def wait(self, ticket: int):
         """Block until frame `ticket` is done: its (H, W) u8 disparity (pinned memory, valid until
         release), plus the f64 cm distance map when the stream computes it on the device."""
+        self._require_open()
         dp, xp = ctypes.c_void_p(), ctypes.c_void_p()
         _lib.check("usv_frame_stream_wait",
                    self._lib.usv_frame_stream_wait(self._h, ticket, ctypes.byref(dp),
                                                    ctypes.byref(xp) if self.device_distance else None))
-        disp = _view(dp.value, (self.H, self.W), np.uint8)
+        disp = _view(self, dp.value, (self.H, self.W), np.uint8)
         if self.device_distance:
-            return disp, _view(xp.value, (self.H, self.W), np.float64)
+            return disp, _view(self, xp.value, (self.H, self.W), np.float64)
         return disp
 
     def release(self, ticket: int) -> None:
+        self._require_open()
         _lib.check("usv_frame_stream_release", self._lib.usv_frame_stream_release(self._h, ticket))
 
 
