@@ -149,7 +149,7 @@ def test_stream_views_outlive_the_stream_object(gpu):
     gc.collect()
     assert np.array_equal(disp, ref)
     fs = FrameStream(W, H, D, w, depth=2)
-    sl, _ = fs.next_inputs()
+    sl = fs.next_inputs()[0]  # (the R staging view is dropped at once)
     view = fs.wait(fs.submit(L, R))[10:20]
     fs.close()  # deferred: sl and view are alive
     gc.collect()
