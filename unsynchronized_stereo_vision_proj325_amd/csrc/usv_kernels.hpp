@@ -55,6 +55,14 @@ struct MatchArgs {
 bool fast_path_supported(const MatchArgs& a);
 hipError_t launch_fast(const MatchArgs& a, hipStream_t s);
 
+// Paired-disparity kernel (usv_sad_pair.hip): SAD, even D > 64, 11 <= w <= 15 (configs C, D, E), on
+// shapes fast_path_supported accepts.  hipErrorInvalidValue otherwise.
+bool pair_path_supported(const MatchArgs& a);
+hipError_t launch_pair(const MatchArgs& a, hipStream_t s);
+
+// SSD kernel (usv_sad_ssd.hip): 11 <= w <= 15, on shapes fast_path_supported accepts.
+hipError_t launch_ssd(const MatchArgs& a, hipStream_t s);
+
 // Grouped paired-disparity kernel for small disparity ranges (usv_sad_group.hip): SAD, even
 // 16 < D <= 64, 5 <= w <= 9, on shapes fast_path_supported accepts.  hipErrorInvalidValue otherwise.
 bool group_path_supported(const MatchArgs& a);

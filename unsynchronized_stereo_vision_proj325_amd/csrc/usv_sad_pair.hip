@@ -1,0 +1,725 @@
+// usv_sad_pair.hip -- the headline block-match kernel on gfx950: SAD with lane = two adjacent
+// disparities (sad_pair_kernel; even D > 64, 11 <= w <= 15: configs C, D, E).
+//
+// Spec: SURVEY.md §8(a) A1 (restated in oracle/sad_oracle.c); DESIGN.md §3 has the derivation.  The
+// reference has no block matcher; its nearest primitive is the u8 absdiff motion mask
+// at P/Main.cpp:304.  Integer arithmetic only: bit-exact with the oracle by construction.
+#include "usv_sad_common.hpp"
+
+namespace usv {
+namespace {
+
+// ===================================================================================
+// Paired-disparity kernel (D > 64, even D, 5 <= r <= 7): lane = two ADJACENT disparities.
+//
+// Lane l of wave w owns d = 2 (64 w + l) in the low half of its packed-u16 sums and
+// d + 1 in the high half, for K = 8 output columns (wave w: disparities [128 w, 128 w + 128)).  The two share the L byte of each
+// chain step (one SGPR for both v_sad_u8 and v_sad_hi_u8) and their R bytes are adjacent
+// columns of the staged row: step j reads entries j (d + 1) and j + 1 (d), so a lane reads
+// K + 2r + 1 staged entries for 2 x K (column, disparity) pairs per step instead of
+// K + 2r for K, and a whole 128-disparity search is ONE wave: per (pixel, disparity) half
+// the L-byte extraction, row addressing and LDS-DMA instructions of the column-paired
+// kernel above, ~30 % less LDS traffic, and no cross-wave combine barrier at D <= 128.
+// Keys: lo = (cost << 8) | d, hi = (cost << 8) | (d + 1); the transpose gives lane
+// 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
+// rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
+// ===================================================================================
+#ifndef USV_PAIR_PIPE
+#define USV_PAIR_PIPE 1  // argmin transpose of row t finished during row t + 1 (latency hidden by the chain)
+#endif
+#ifndef USV_NT_DIST
+#define USV_NT_DIST 0  // experiment: the paired kernel's distance map through non-temporal stores
+#endif
+#ifndef USV_WIDE_FLUSH
+#define USV_WIDE_FLUSH 1  // paired kernel: one 8-byte disparity store and one 16-byte distance store per lane per chunk
+#endif
+#ifndef USV_PAIR_PIPE_R7
+#define USV_PAIR_PIPE_R7 0  // experiment: pipelined argmin at r = 7 (needs USV_PAIR_OCC7=2, USV_PAIR_SPLIT_R=8)
+#endif
+template <int RAD>
+constexpr bool kPairPipe = USV_PAIR_PIPE && (RAD == 5 || (RAD == 7 && USV_PAIR_PIPE_R7));
+template <int RAD, int NW>
+struct PCfg {
+    static constexpr int K = 8;
+    static constexpr int WIN = 2 * RAD + 1;
+    static constexpr int NPOS = K + 2 * RAD;            // chain steps
+    static constexpr int NE = NPOS + 1;                 // staged entries a lane reads per row
+    static constexpr int VEC = 2;                       // lane offsets are 2 entries apart
+    static constexpr int NE_V = (NE + VEC - 1) / VEC * VEC;
+    static constexpr int NR = 2 * 63 + NE_V;            // entries a wave stages per row
+    static constexpr int NQ = (NR + 63) / 64;           // DMA instructions per row
+    static constexpr int NRS = NQ * 64;
+    static constexpr int NB = 8;                        // ring slots per wave
+#ifndef USV_PAIR_SPLIT_R
+#define USV_PAIR_SPLIT_R 7  // radius from which the row's entries are read in two batches
+#endif
+    static constexpr int SPLIT = RAD >= USV_PAIR_SPLIT_R ? 2 : 1;
+    static constexpr int PD = NB - 1;
+    static constexpr int KRB = WIN;
+    static constexpr int RBUF_OFF = 0;
+    static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
+    static constexpr int TB_WORDS = K * 64;
+    static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
+    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
+    static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
+    static_assert(RAD >= 2 && RAD <= 7, "paired kernel: 5 <= w <= 15");
+    static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
+    static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
+};
+
+template <int RAD, int NW, int EDGE>
+__device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                               uint8_t* __restrict__ disp, double* __restrict__ dist,
+                                               const MatchArgs& a, uint32_t* smem, int lane, int wave, int x0,
+                                               int y_begin, int y_end) {
+    using C = PCfg<RAD, NW>;
+    using LS = LSeg<RAD, EDGE, C::K>;
+    using LWords = typename SWords<LS::NLD>::T;
+    constexpr int WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, KRB = C::KRB, NPOS = C::NPOS;
+    constexpr int NDMA = C::NQ;
+    // lane l owns (d, d + 1), d = 2 (64 wave + l); lanes past the last full pair replay it
+    const int lmax = min(63, a.D / 2 - 1 - 64 * wave);
+    const int l_eff = min(lane, lmax);
+    const int dwave = 128 * wave;
+    const int cbase = x0 - RAD - (dwave + 2 * 63 + 1);  // first R column this wave stages
+    uint32_t* rbuf = smem + C::RBUF_OFF + wave * NB * C::NRS;
+    uint32_t* comb = smem + C::COMB_OFF;
+    uint32_t* tb = smem + C::TB_OFF + wave * C::TB_WORDS;
+    // transposed reads: lane m = 8p + q takes words 64 p + 8 q .. + 7 as two 16-B windows.  A
+    // ds_read_b128 is serviced in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32)
+    // over 64 banks, and window w of lane (p, q) sits on banks 8 q + 4 w: visiting the windows in
+    // the order w = j ^ ((q >> 2) ^ (p >> 1)) gives the 16 lanes of every group 16 distinct
+    // 4-bank slots (no conflict; without the p term two lanes of each group collide).
+    uint32_t rdw[2], dlo[2], dhi[2];
+    {
+        const int p = lane >> 3, q = lane & 7, rot = ((q >> 2) ^ (p >> 1)) & 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int win = j ^ rot;
+            rdw[j] = (uint32_t)(16 * p + 2 * q + win);  // uint4 index: (64 p + 8 q + 4 win) / 4
+            // source lanes past lmax replay lane lmax's data: the same cost with a larger d, so
+            // their keys never win and their d bytes need no clamp (max 2 (64 + 63) + 1 = 255)
+            uint32_t lo = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int src = 8 * q + 4 * win + e;
+                lo |= (uint32_t)(dwave + 2 * src) << (8 * e);
+            }
+            dlo[j] = lo;
+            dhi[j] = lo + 0x01010101u;  // d even: + 1 per byte, no carry
+        }
+    }
+    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
+    const int s_l = 2 * (63 - l_eff);  // this lane's first staged entry
+    const int nout = y_end - y_begin;
+    const int T = nout + 2 * RAD;
+    const int Hm1 = a.H - 1, Wm1 = a.W - 1;
+    auto row_off = [&](int t) -> uint32_t {
+        const int y = min(max(y_begin - RAD + t, 0), Hm1);
+        return (uint32_t)(y * a.pitch);
+    };
+    const uint8_t* const Lseg = L + LS::base(x0);
+    const uint8_t* const Rdma = R - kDmaBias;
+    const int y0 = y_begin - RAD;
+    const int last_off = Hm1 * a.pitch;
+    int rawL = (y0 + WIN + 1) * a.pitch, rawR = (y0 + WIN + PD) * a.pitch;
+    const su4 rsrc = [&] {
+        const uint64_t base = reinterpret_cast<uint64_t>(Rdma);
+        su4 r;
+        r[0] = (uint32_t)base;
+        r[1] = (uint32_t)(base >> 32);
+        r[2] = 0xFFFFFFFFu;
+        r[3] = 0x00020000u;
+        return r;
+    }();
+    uint32_t colRb[C::NQ];
+#pragma unroll
+    for (int i = 0; i < C::NQ; ++i)
+        colRb[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1) + kDmaBias - 256u * (uint32_t)i;
+    const uint32_t rbase = lds_addr(rbuf);
+    auto issue_dma = [&](int t) {
+        const int buf = t & (NB - 1);
+        dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+    };
+    LWords lw_next;
+    auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
+
+    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
+        constexpr bool WARM = decltype(warm_tag)::value;
+        constexpr int I = decltype(i_tag)::value;
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        wait_vmcnt<(PD - 1) * NDMA>();
+        __builtin_amdgcn_wave_barrier();
+        if constexpr (WARM) {
+            issue_dma(t + PD);
+        } else {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));
+            const int buf = (t + PD) & (NB - 1);
+            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            rawR = rr + a.pitch;
+        }
+        // (pipelined argmin: the ring row leaving the window is subtracted first, so its registers
+        // are free for this row's staged entries -- no copies)
+        constexpr bool EARLY_SUB = !WARM && kPairPipe<RAD>;
+        if constexpr (EARLY_SUB) {
+#pragma unroll
+            for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        }
+        uint32_t Lv[NPOS];
+        {
+            wait_lgkm0_pin<LS::NLD>(lw_next);
+            LWords cur = lw_next;
+            uint32_t lw[8];
+            unpack_words<LS::NLD>(cur, lw);
+#pragma unroll
+            for (int j = 0; j < NPOS; ++j) {
+                const int bidx = LS::byte(j);
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+                else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+            }
+        }
+        auto lbyte = [&](int j) -> uint32_t { return Lv[j]; };
+        using VT = typename VecT<C::VEC>::T;
+        int boff = (t & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
+        // The staged entries come in C::SPLIT batches of vector reads, each consumed by the chain
+        // steps it completes before the next batch is read (r = 7: fewer live VGPRs, so three
+        // waves fit per SIMD; the second batch's latency is covered by the other waves).
+        uint32_t E[C::NE_V];
+        constexpr int NV = C::NE_V / C::VEC, NV1 = C::SPLIT > 1 ? (NV + 1) / 2 : NV;
+        constexpr int J1 = C::SPLIT > 1 ? NV1 * C::VEC - 1 : NPOS;  // steps the first batch completes
+#pragma unroll
+        for (int k = 0; k < NV1; ++k) {
+            const VT v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+        // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half).  With the argmin
+        // pipelined, piece j of the previous row's argmin follows chain step j and the pair is
+        // fenced: the two independent dependency chains interleave instruction by instruction.
+        uint32_t A[NPOS + 1];
+        A[0] = 0;
+        auto chain_step = [&](auto jt) {
+            constexpr int j = decltype(jt)::value;
+            const uint32_t l = lbyte(j);
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            pre(jt);
+            if constexpr (EARLY_SUB) __builtin_amdgcn_sched_barrier(0);
+        };
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (chain_step(std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, J1>{});
+        if constexpr (C::SPLIT > 1) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = NV1; k < NV; ++k) {
+                const VT v = rb[k];
+#pragma unroll
+                for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+            }
+#pragma unroll
+            for (int j = J1; j < NPOS; ++j)
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(lbyte(j), E[j], __builtin_amdgcn_sad_u8(lbyte(j), E[j + 1], A[j]));
+        }
+#pragma unroll
+        for (int x = 0; x < K; ++x) {
+            const uint32_t h = A[x + WIN] - A[x];  // both halves in [0, 65535], no borrow
+            if constexpr (WARM || EARLY_SUB) S[x] = S[x] + h;
+            else S[x] = (S[x] - ring[I][x]) + h;
+            ring[I][x] = h;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (WARM) {
+            load_lw(t + 1);
+        } else {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    int cb = 0, y_chunk = y_begin;
+    // Wide flush (USV_WIDE_FLUSH): a chunk's outputs leave in two store instructions -- lane r
+    // writes row r's 8 disparity bytes as one 8-byte store, lane 4r + q row r's distances 2q, 2q+1
+    // as one 16-byte store -- instead of a byte + a double per lane and item (4 per 11-row chunk).
+    // Global stores count in vmcnt on gfx9 with the LDS-DMA look-ahead, so fewer, wider stores also
+    // hold up fewer of the next rows' counted DMA waits.  Needs 4-byte aligned disparity rows.
+    const bool wide = USV_WIDE_FLUSH && ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
+    auto flush = [&](int rows) {
+        if constexpr (NW > 1) lds_barrier();
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        if (wide) {
+            static_assert(K == 8, "one 8-byte disparity store per row");
+            const uint32_t* crow = comb + (cb * KRB) * NW * K;
+            if (tid < rows) {
+                uint4 k0 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[0];
+                uint4 k1 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[1];
+#pragma unroll
+                for (int w2 = 1; w2 < NW; ++w2) {
+                    const uint4 m0 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[0];
+                    const uint4 m1 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[1];
+                    k0 = make_uint4(min(k0.x, m0.x), min(k0.y, m0.y), min(k0.z, m0.z), min(k0.w, m0.w));
+                    k1 = make_uint4(min(k1.x, m1.x), min(k1.y, m1.y), min(k1.z, m1.z), min(k1.w, m1.w));
+                }
+                // byte 0 of each key is its disparity
+                const uint32_t lo = __builtin_amdgcn_perm(k0.y, k0.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k0.w, k0.z, 0x04000c0cu);
+                const uint32_t hi = __builtin_amdgcn_perm(k1.y, k1.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k1.w, k1.z, 0x04000c0cu);
+                const size_t y = (size_t)(y_chunk + tid);
+                *reinterpret_cast<uint2*>(disp + y * a.disp_pitch + x0) = make_uint2(lo, hi);
+            }
+            if (dist && tid < 4 * rows) {
+                struct __attribute__((aligned(8))) D2 { double a, b; };
+                const int r = tid >> 2, q = tid & 3;
+                uint2 kk = reinterpret_cast<const uint2*>(crow + r * NW * K)[q];
+#pragma unroll
+                for (int w2 = 1; w2 < NW; ++w2) {
+                    const uint2 m = reinterpret_cast<const uint2*>(crow + (r * NW + w2) * K)[q];
+                    kk = make_uint2(min(kk.x, m.x), min(kk.y, m.y));
+                }
+                const size_t y = (size_t)(y_chunk + r);
+                if constexpr (USV_NT_DIST) {  // experiment: write-once map as non-temporal stores
+                        typedef double v2d __attribute__((ext_vector_type(2)));
+                        v2d v = {lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+                        __builtin_nontemporal_store(v, reinterpret_cast<v2d*>(dist + y * a.dist_pitch + x0 + 2 * q));
+                    } else {
+                        *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
+                    }
+            }
+            y_chunk += rows;
+            cb ^= 1;
+            return;
+        }
+        const int items = rows * K;
+        for (int i = tid; i < items; i += NW * 64) {
+            const int row = i / K, p = i - row * K;
+            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
+            const uint32_t dv = key & 0xFFu;
+            const size_t y = (size_t)(y_chunk + row);
+            disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
+            if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
+        }
+        y_chunk += rows;
+        cb ^= 1;
+    };
+    // Argmin of one row, in two halves so that the LDS round trip of the transpose and the
+    // dependent min / DPP tail overlap the next row's chain (USV_PAIR_PIPE):
+    //   tr_issue:  lane l stores its 8 packed words, lane 8p + q reads the 8 words of pixel p from
+    //              lanes 8q .. 8q + 7 (two ds_read_b128) -- nothing waits on them here;
+    //   tr_finish: 16 keys (cost << 8) | d by v_perm, a v_min3 tree, three DPP rounds across the 8
+    //              lanes of the pixel, one comb word per pixel.
+    uint4 trq[2];
+    auto tr_issue = [&](const uint32_t(&S)[K]) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            // (r = 7: the second window's index is rebuilt per row as well)
+            const uint32_t ri = (C::SPLIT > 1 && j == 1) ? (rdw[0] ^ 1u) : rdw[j];
+            trq[j] = reinterpret_cast<const uint4*>(tb)[ri];
+        }
+        asm volatile("" ::: "memory");
+    };
+    // tr_finish in 16 pieces (piece J after chain step J of the next row when pipelined)
+    uint32_t fv[16], fb[5], fm;
+    auto tr_piece = [&](auto jt, int slot) {
+        constexpr int J = decltype(jt)::value;
+        if constexpr (J < 8) {
+            constexpr int j = J >> 2, e = J & 3;
+            const uint32_t w = e == 0 ? trq[j].x : e == 1 ? trq[j].y : e == 2 ? trq[j].z : trq[j].w;
+            // (r = 7: the second window's d table and both d + 1 tables are rebuilt per row from
+            // dlo[0], three VGPRs fewer across the loop: bit 3 of every d byte is the window)
+            uint32_t dl = dlo[j], dh = dhi[j];
+            if constexpr (C::SPLIT > 1) {
+                dl = j == 0 ? dlo[0] : (dlo[0] ^ 0x08080808u);
+                dh = dl + 0x01010101u;
+            }
+            fv[8 * j + 2 * e] = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
+            fv[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
+        } else if constexpr (J == 8) {
+            fb[0] = min(min(fv[0], fv[1]), fv[2]);
+            fb[1] = min(min(fv[3], fv[4]), fv[5]);
+        } else if constexpr (J == 9) {
+            fb[2] = min(min(fv[6], fv[7]), fv[8]);
+            fb[3] = min(min(fv[9], fv[10]), fv[11]);
+        } else if constexpr (J == 10) {
+            fb[4] = min(min(fv[12], fv[13]), fv[14]);
+            fb[0] = min(min(fb[0], fb[1]), fb[2]);
+        } else if constexpr (J == 11) {
+            fb[3] = min(min(fb[3], fb[4]), fv[15]);
+            fm = min(fb[0], fb[3]);
+        } else if constexpr (J == 12) {
+            fm = min(fm, dpp<kQuadSwap1>(fm));
+        } else if constexpr (J == 13) {
+            fm = min(fm, dpp<kQuadSwap2>(fm));
+        } else if constexpr (J == 14) {
+            fm = min(fm, dpp<kRowHalfMirror>(fm));
+        } else if constexpr (J == 15) {
+            int px = lane >> 3;
+            if constexpr (C::SPLIT > 1) {  // r = 7: rebuilt, not kept live through the row loop
+                px = threadIdx.x;
+                asm volatile("" : "+v"(px));
+                px = (px & 63) >> 3;
+            }
+            comb[((cb * KRB + slot) * NW + wave) * K + px] = fm;
+        }
+    };
+    auto tr_finish = [&](int slot) {
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (tr_piece(std::integral_constant<int, J>{}, slot), ...);
+        }(std::make_integer_sequence<int, 16>{});
+    };
+    auto emit = [&](const uint32_t(&S)[K], int slot) {
+        tr_issue(S);
+        tr_finish(slot);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto no_pre = [](auto) {};
+
+    // ---- prefetched row boundary (USV_PAIR_PREF, pipelined r = 5 only) ----
+    // Without it every row starts with an s_waitcnt lgkmcnt(0) (the pinned L words are a scalar
+    // load, which returns out of order) that also retires the previous row's transpose reads issued
+    // just before, then issues its staged-entry reads and waits for the first of them: two LDS round
+    // trips per row with nothing else of this wave to issue.  Here the boundary is reordered:
+    //   end of row t:  lgkmcnt(0) (everything of row t, and the L words of row t + 1 loaded a row
+    //                  earlier) -> extract row t + 1's L bytes -> [flush] -> scalar-load row t + 2's
+    //                  L words -> vmcnt wait for row t + 1's DMA -> the first PV vector reads of
+    //                  row t + 1's staged entries -> row t's transpose WRITES;
+    //   row t + 1:     DMA, ring subtraction, the remaining entry reads, THEN the transpose reads,
+    //                  the chain (its first steps run on the prefetched entries) with the argmin
+    //                  pieces from step PIECE_OFF on, so the transpose reads have a whole run of
+    //                  chain steps to land.
+#ifndef USV_PAIR_PREF
+#define USV_PAIR_PREF 0  // vector reads of the next row prefetched (0 = off)
+#endif
+#ifndef USV_PAIR_PIECE_OFF
+#define USV_PAIR_PIECE_OFF 8  // chain step of the first argmin piece (USV_PAIR_PREF)
+#endif
+    constexpr bool PREF = USV_PAIR_PREF > 0 && kPairPipe<RAD> && C::SPLIT == 1;
+    using VTp = typename VecT<C::VEC>::T;
+    constexpr int NVp = C::NE_V / C::VEC;
+    constexpr int PV = PREF ? (USV_PAIR_PREF < NVp ? USV_PAIR_PREF : NVp) : 1;
+    constexpr int OFFP = USV_PAIR_PIECE_OFF;
+    uint32_t Epf[PV * C::VEC];
+    uint32_t Lv[NPOS];  // L bytes of the row about to run
+    auto extract_l = [&]() {  // after wait_lgkm0_pin(lw_next)
+        LWords cur = lw_next;
+        uint32_t lw[8];
+        unpack_words<LS::NLD>(cur, lw);
+#pragma unroll
+        for (int j = 0; j < NPOS; ++j) {
+            const int bidx = LS::byte(j);
+            if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
+            else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+        }
+    };
+    auto prefetch_e = [&](int t_next) {
+        wait_vmcnt<(PD - 1) * NDMA>();  // row t_next's DMA (issued PD rows ago) has landed
+        __builtin_amdgcn_wave_barrier();
+        int boff = (t_next & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const VTp v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) Epf[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+    };
+    auto tr_write = [&](const uint32_t(&S)[K]) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        asm volatile("" ::: "memory");
+    };
+    auto tr_read = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) trq[j] = reinterpret_cast<const uint4*>(tb)[rdw[j]];
+        asm volatile("" ::: "memory");
+    };
+    auto do_row_pref = [&](int t_in, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
+        constexpr int I = decltype(i_tag)::value;
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));
+            const int buf = (t + PD) & (NB - 1);
+            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            rawR = rr + a.pitch;
+        }
+#pragma unroll
+        for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        uint32_t E[C::NE_V];
+#pragma unroll
+        for (int e = 0; e < PV * C::VEC; ++e) E[e] = Epf[e];
+        int boff = (t & (NB - 1)) * C::NRS;
+        asm volatile("" : "+s"(boff));
+        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
+#pragma unroll
+        for (int k = PV; k < NVp; ++k) {
+            const VTp v = rb[k];
+#pragma unroll
+            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+        }
+        tr_read();
+        uint32_t A[NPOS + 1];
+        A[0] = 0;
+        auto chain_step = [&](auto jt) {
+            constexpr int j = decltype(jt)::value;
+            const uint32_t l = Lv[j];
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            if constexpr (j >= OFFP && j - OFFP < 16) tr_piece(std::integral_constant<int, j - OFFP>{}, I);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (chain_step(std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, NPOS>{});
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            ((J >= (NPOS - OFFP > 0 ? NPOS - OFFP : 0) ? tr_piece(std::integral_constant<int, J>{}, I) : void()), ...);
+        }(std::make_integer_sequence<int, 16>{});
+#pragma unroll
+        for (int x = 0; x < K; ++x) {
+            const uint32_t h = A[x + WIN] - A[x];
+            S[x] = S[x] + h;
+            ring[I][x] = h;
+        }
+    };
+    auto row_tail = [&](int t, bool do_flush, const uint32_t(&S)[K]) {
+        wait_lgkm0_pin<LS::NLD>(lw_next);
+        extract_l();
+        if (do_flush) flush(KRB);
+        {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        }
+        prefetch_e(t + 1);
+        tr_write(S);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    uint32_t S[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) S[i] = 0;
+    uint32_t ring[WIN][K];
+    static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
+    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
+    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
+    load_lw(0);
+    using WarmT = std::integral_constant<bool, true>;
+    using SteadyT = std::integral_constant<bool, false>;
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring, no_pre), ...);
+    }(std::make_integer_sequence<int, WIN>{});
+    // Pipelined argmin (PIPE): output row k is slot k % KRB.  Row k's transpose is issued after its
+    // chain and finished inside the next row's do_row (after that row's staged reads are issued), so
+    // slot I is pending when the I-th row of a WIN-row group starts; the chunk is flushed once slot
+    // KRB - 1 is finished.  (r = 6, 7 keep the unpipelined order: the held transpose words spill.)
+    constexpr bool PIPE = kPairPipe<RAD>;
+    static_assert(KRB == WIN, "pending slot = row index in the unrolled group");
+    static_assert(!PIPE || NPOS >= 16, "16 argmin pieces ride on the chain steps");
+    if constexpr (PREF) {
+        row_tail(WIN - 1, false, S);
+    } else if constexpr (PIPE) {
+        tr_issue(S);
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+        emit(S, 0);
+    }
+    auto step = [&](int t0, auto i_tag) {
+        constexpr int I = decltype(i_tag)::value;
+        if constexpr (PREF) {
+            do_row_pref(t0 + I, i_tag, S, ring);
+            row_tail(t0 + I, I == KRB - 1, S);
+        } else if constexpr (PIPE) {
+            do_row(t0 + I, SteadyT{}, i_tag, S, ring, [&](auto jt) {
+                if constexpr (decltype(jt)::value < 16) tr_piece(jt, I);
+            });
+            if constexpr (I == KRB - 1) flush(KRB);
+            tr_issue(S);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            do_row(t0 + I, SteadyT{}, i_tag, S, ring, no_pre);
+            emit(S, (I + 1) % WIN);
+            if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+        }
+    };
+    for (int t0 = WIN; t0 < T; t0 += WIN) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            bool go = true;
+            ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
+        }(std::make_integer_sequence<int, WIN>{});
+    }
+    wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
+    if constexpr (PIPE) {
+        const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
+        if constexpr (PREF) tr_read();
+        tr_finish(last);
+        if (last == KRB - 1) flush(KRB);
+    }
+    const int rest = nout % KRB;
+    if (rest) flush(rest);
+    wait_vmcnt<0>();
+}
+
+#ifndef USV_PAIR_OCC7
+#define USV_PAIR_OCC7 3  // waves per SIMD the r = 7 paired kernel is compiled for
+#endif
+#ifndef USV_PAIR_OCC5
+#define USV_PAIR_OCC5 3  // waves per SIMD the r <= 6 paired kernel is compiled for
+#endif
+constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : USV_PAIR_OCC5; }
+
+template <int RAD, int NW>
+__global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
+                                                              const uint8_t* __restrict__ R,
+                                                              uint8_t* __restrict__ disp,
+                                                              double* __restrict__ dist, MatchArgs a, BandPlan P) {
+    using C = PCfg<RAD, NW>;
+    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the work map of sad_fast_kernel (XCD-contiguous tile runs, generation-weighted bands)
+    const unsigned total = gridDim.x, lin = blockIdx.x;
+    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
+    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
+    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
+    const bool past = tile >= per_pair && P.extra > 0;
+    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
+    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
+    const unsigned pair = past ? 0u : tile / per_pair;
+    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
+    const unsigned long_run = base + 1u, split = rem * long_run;
+    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
+                                  (unsigned)P.gen_g, P.weights);
+    const unsigned pre = bs.pre, tot = bs.tot;
+    const int xt = (int)col_xt;
+    const int n_xt = P.n_xt;
+    int x0 = xt * C::K;
+    if (xt == n_xt - 1) x0 = a.W - C::K;
+    else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
+    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
+    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
+    L += (size_t)pair * a.pair_stride;
+    R += (size_t)pair * a.pair_stride;
+    disp += (size_t)pair * a.disp_stride;
+    if (dist) dist += (size_t)pair * a.dist_stride;  // (the table is staged inside the band loop)
+    if (y_end <= y_begin) return;
+    if (xt == 0)
+        pair_band_loop<RAD, NW, kLeft>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    else if (xt == n_xt - 1)
+        pair_band_loop<RAD, NW, kRight>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+    else
+        pair_band_loop<RAD, NW, kInterior>(L, R, disp, dist, a, smem, lane, wave, x0, y_begin, y_end);
+}
+
+template <int RAD, int NW>
+int resident_pair_blocks_per_cu() {
+    static const int n = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair_kernel<RAD, NW>, NW * 64, 0) != hipSuccess ||
+            v <= 0)
+            v = 1;
+        return v;
+    }();
+    return n;
+}
+
+// Generation weights of the paired kernel (one-wave workgroups, three generations per SIMD):
+// interleaved A/B on config C, 100:90:70 / 100:80:58 / 100:85:55 / 100:80:50 / 100:75:50 /
+// 100:70:45 = 69.75 / 68.61 / 67.63 / 67.42 / 67.27 / 68.25 us (profiles/probes_r02/ab_pair_weights_*).
+// Re-fitted after the argmin was pipelined into the next row's chain (two A/B runs on two boxes, 4 rounds
+// each): 100:75:50 65.3 / 65.0, 100:70:45 64.4 / 64.7, 100:70:40 64.6, 100:65:40 66.3, 100:60:35 68.5,
+// 100:80:55 66.2, 100:85:60 66.6 us (profiles/probes_r02/ab_pair_weights_3_r02.txt).
+// Config E (r = 7, argmin not pipelined) keeps 100:75:50: 617.0 vs 639.9 us with 100:70:45 (same A/B run).
+#ifndef USV_PAIR_GEN_WEIGHTS
+#define USV_PAIR_GEN_WEIGHTS 0x2D2D4664u  // 100, 70, 45, 45: pipelined argmin (r = 5)
+#endif
+#ifndef USV_PAIR_GEN_WEIGHTS_UNPIPED
+#define USV_PAIR_GEN_WEIGHTS_UNPIPED 0x32324B64u  // 100, 75, 50, 50: r = 6, 7 with one-wave workgroups
+#endif
+// Two-wave workgroups (D > 128: config E) want flatter heights (three interleaved A/B runs of 3 rounds on
+// config E): 100:75:50 620-625, 100:65:40 684, 100:80:60 570, 100:85:60 568, 100:85:65 553-555,
+// 100:85:70 555, 100:90:70 557, 100:90:80 565, 100:95:85 570, uniform 573 us
+// (profiles/probes_r02/ab_pair_weights_E_r02.txt).
+#ifndef USV_PAIR_GEN_WEIGHTS_NW2
+#define USV_PAIR_GEN_WEIGHTS_NW2 0x41415564u  // 100, 85, 65, 65
+#endif
+
+template <int RAD, int NW>
+hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
+    constexpr int K = PCfg<RAD, NW>::K, WIN = 2 * RAD + 1;
+    BandPlan P{};
+    P.n_xt = (a.W + K - 1) / K;
+    const int per_cu = resident_pair_blocks_per_cu<RAD, NW>();
+    const long slots = (long)cu_count() * per_cu;
+    const long NC = (long)P.n_xt * a.batch;
+    long m = slots / NC;
+    if (m < 1) m = 1;
+    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    if (m > m_max) m = m_max;
+    P.m = (int)m;
+    const long ex = slots - NC * m;
+    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    const long total = NC * m + P.extra;
+    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+#ifndef USV_PAIR_GEN_G_X4
+#define USV_PAIR_GEN_G_X4 4  // experiment knob: generation size x4/4 (4 = one generation per SIMD-wave slot)
+#endif
+    P.gen_g = (int)((4L * (cu_count() / 8)) * USV_PAIR_GEN_G_X4 / (4 * NW));
+    if (P.gen_g < 1) P.gen_g = 1;
+    const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
+    P.weights = !three ? 0x01010101u
+              : NW > 1 ? USV_PAIR_GEN_WEIGHTS_NW2
+              : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
+    dim3 grid((unsigned)total), block(NW * 64);
+    hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
+    return hipGetLastError();
+}
+
+#ifndef USV_PAIR
+#define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
+#endif
+#ifndef USV_PAIR_SMALL
+#define USV_PAIR_SMALL 0  // experiment: the paired kernel also for even 32 < D <= 64 and 5 <= w <= 9
+#endif
+bool pair_supported(const MatchArgs& a) {
+    if (USV_PAIR_SMALL && a.D > 32 && a.D <= 64 && (a.D % 2) == 0 && a.w >= 5 && a.w <= 9) return true;
+    return USV_PAIR && a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15;
+}
+template <int RAD>
+hipError_t launch_pair_r(const MatchArgs& a, hipStream_t s) {
+    return a.D <= 128 ? launch_pair_rn<RAD, 1>(a, s) : launch_pair_rn<RAD, 2>(a, s);
+}
+
+}  // namespace
+
+bool pair_path_supported(const MatchArgs& a) { return pair_supported(a); }
+
+hipError_t launch_pair(const MatchArgs& a, hipStream_t s) {
+    if (!pair_supported(a)) return hipErrorInvalidValue;
+    switch ((a.w - 1) / 2) {
+#if USV_PAIR_SMALL
+        case 2: return launch_pair_r<2>(a, s);
+        case 3: return launch_pair_r<3>(a, s);
+        case 4: return launch_pair_r<4>(a, s);
+#endif
+        case 5: return launch_pair_r<5>(a, s);
+        case 6: return launch_pair_r<6>(a, s);
+        case 7: return launch_pair_r<7>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace usv
