@@ -32,7 +32,7 @@ class _PinnedView:
     """Array interface over a FrameStream's pinned memory that holds a reference to the stream: a numpy
     view's base is this object, so while any view (or a slice of one) is alive the stream -- and the
     pinned allocation behind it -- cannot be collected, and an explicit close() defers the free until
-    the last view is gone (FrameStream._views)."""
+    the last view is gone (FrameStream._nviews)."""
 
     def __init__(self, owner, ptr: int, shape, dtype):
         self._owner = owner
@@ -42,7 +42,8 @@ class _PinnedView:
 
 def _view(owner, ptr: int, shape, dtype) -> np.ndarray:
     holder = _PinnedView(owner, ptr, shape, dtype)
-    owner._views.add(holder)
+    owner._nviews += 1
+    weakref.finalize(holder, owner._view_gone)
     return np.asarray(holder)
 
 
@@ -52,7 +53,7 @@ class FrameStream:
     def __init__(self, W: int, H: int, D: int = 128, w: int = 11, metric: str = "sad", depth: int = 3,
                  device_distance: bool = False):
         self._lib = _lib.load()
-        self._views = weakref.WeakSet()  # live _PinnedView holders (numpy views of the pinned staging)
+        self._nviews = 0  # live _PinnedView holders (numpy views of the pinned staging)
         self._closing = False
         self.W, self.H, self.D, self.w = W, H, D, w
         self.device_distance = device_distance
@@ -67,17 +68,12 @@ class FrameStream:
         next_inputs() / wait() are still alive the free is deferred until the last one is collected,
         so a view can never point at released memory; the stream takes no new submits meanwhile."""
         self._closing = True
-        if not self._h:
-            return
-        live = list(self._views)
-        if live:
-            for holder in live:
-                weakref.finalize(holder, self._destroy_if_unviewed)
-            return
-        self._destroy()
+        if self._h and self._nviews == 0:
+            self._destroy()
 
-    def _destroy_if_unviewed(self) -> None:
-        if self._h and not len(self._views):
+    def _view_gone(self) -> None:  # a view's holder was collected
+        self._nviews -= 1
+        if self._closing and self._nviews == 0 and self._h:
             self._destroy()
 
     def _destroy(self) -> None:
