@@ -302,6 +302,23 @@ usv_status usv_contour_pair_scores(const double* desc_a, int n_a, const double* 
                                    void* stream);
 
 /*
+ * GenerateMatchingList on the device from HOST inputs and into a HOST list (the drop-in form of
+ * usv_generate_matching_list; same arguments, same output order and capacity rule, scores equal to
+ * the host restatement's within the device log10 rounding).  The matcher object owns pinned staging,
+ * device buffers for up to max_contours contours and max_points points per set, and a stream: one call
+ * = one H2D copy, three launches (descriptors of each set; one wave per row of the score matrix keeps
+ * v < 0.75 and compacts the row in j order with a ballot), one D2H copy, a host concatenation of the
+ * rows in i order.  The current device at create time is the matcher's device; not thread-safe (one
+ * object per caller thread).  Replaces the per-pair loop of P/Main.cpp:403-426.
+ */
+typedef struct usv_contour_matcher usv_contour_matcher;
+usv_status usv_contour_matcher_create(int max_contours, int max_points, usv_contour_matcher** out);
+usv_status usv_contour_matcher_destroy(usv_contour_matcher* m);
+usv_status usv_generate_matching_list_gpu(usv_contour_matcher* m, const int* pts_a, const int* off_a, int n_a,
+                                          const int* pts_b, const int* off_b, int n_b, usv_match* out, int cap,
+                                          int* n_out);
+
+/*
  * MovingObjectDistanceCalculator over arrays, arguments in the reference's
  * order (P/DistanceCalculator.hpp:37-46).  Points are interleaved float (x, y),
  * triples int (x, y, z), time stamps steady_clock ticks (ns).

@@ -107,6 +107,10 @@ SIGNATURES = {
     "usv_contour_area": (c_double, [POINTER(c_int), c_int]),
     "usv_contour_descriptors": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "usv_contour_pair_scores": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "usv_contour_matcher_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "usv_contour_matcher_destroy": (c_int, [c_void_p]),
+    "usv_generate_matching_list_gpu": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), c_int, POINTER(c_int),
+                                               POINTER(c_int), c_int, POINTER(usv_match), c_int, POINTER(c_int)]),
     "usv_min_area_rect": (c_int, [POINTER(c_int), c_int, POINTER(c_float)]),
     "usv_match_centroids": (c_int, [POINTER(c_int), POINTER(c_int), c_int, POINTER(usv_match), c_int,
                                     POINTER(c_float), POINTER(c_int)]),

@@ -6,8 +6,9 @@
 each contour's Hu-moment I1 terms and area once on the device
 (``usv_contour_descriptors``) and all N×M scores in one launch
 (``usv_contour_pair_scores``), instead of the reference's per-pair
-recomputation.  The threshold/compaction of the N×M score matrix runs on the
-host after one device-to-host copy (order-preserving, tiny).
+recomputation.  ``ContourMatcherGPU`` (usv_generate_matching_list_gpu) does the
+whole call on the device: one copy in, the descriptor launches, a selection
+launch that keeps v < 0.75 and compacts each row in order, one copy out.
 
 OpenCV 3.0 is absent, so parity with OpenCV itself is UNPINNED; the device
 scores equal the host restatement's to the ulp (log10 is the only libm call,
@@ -52,11 +53,75 @@ def contour_pair_scores(desc_a: torch.Tensor, desc_b: torch.Tensor, stream=None)
     return scores
 
 
+class ContourMatcherGPU:
+    """usv_contour_matcher (include/usv.h): GenerateMatchingList on the device from host contour sets,
+    selection and in-order compaction included, for up to max_contours contours and max_points points
+    per set (pinned staging and device buffers allocated once, on the current HIP device)."""
+
+    def __init__(self, max_contours: int = 512, max_points: int = 1 << 16):
+        import ctypes
+        self._ct = ctypes
+        self.lib = _lib.load()
+        self.max_contours, self.max_points = max_contours, max_points
+        h = ctypes.c_void_p()
+        _lib.check("usv_contour_matcher_create", self.lib.usv_contour_matcher_create(max_contours, max_points,
+                                                                                     ctypes.byref(h)))
+        self.handle = h
+        self._out = (_lib.usv_match * 1)()
+
+    def close(self):
+        if self.handle:
+            _lib.check("usv_contour_matcher_destroy", self.lib.usv_contour_matcher_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fits(self, n_a: int, n_b: int, p_a: int, p_b: int) -> bool:
+        return max(n_a, n_b) <= self.max_contours and max(p_a, p_b) <= self.max_points
+
+    def match_flat(self, pa, oa, pb, ob):
+        """Flattened int32 sets (as usv_generate_matching_list) -> ctypes usv_match array, count."""
+        ct = self._ct
+        n_a, n_b = len(oa) - 1, len(ob) - 1
+        cap = max(1, n_a * n_b)
+        if len(self._out) < cap:
+            self._out = (_lib.usv_match * cap)()
+        n = ct.c_int(0)
+        ip = ct.POINTER(ct.c_int)
+        _lib.check("usv_generate_matching_list_gpu", self.lib.usv_generate_matching_list_gpu(
+            self.handle, pa.ctypes.data_as(ip), oa.ctypes.data_as(ip), n_a, pb.ctypes.data_as(ip),
+            ob.ctypes.data_as(ip), n_b, self._out, cap, ct.byref(n)))
+        return self._out, n.value
+
+    def __call__(self, contours_l, contours_r):
+        pa, oa = _flatten(contours_l)
+        pb, ob = _flatten(contours_r)
+        out, n = self.match_flat(pa, oa, pb, ob)
+        return [(out[k].left_index, out[k].right_index, out[k].match_value) for k in range(n)]
+
+
+_MATCHERS: dict[int, ContourMatcherGPU] = {}
+
+
 def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
-    """Contours as lists of (x, y) int points -> list[(i, j, score)] with score < 0.75 (NaN dropped)."""
+    """Contours as lists of (x, y) int points -> list[(i, j, score)] with score < 0.75 (NaN dropped), i-major
+    then j-minor like GenerateMatchingList (P/Main.cpp:403-426), through the device matcher
+    (usv_generate_matching_list_gpu: one H2D copy, descriptors + selection on the device, one D2H copy).
+    `stream` is unused: the matcher owns its stream and returns host results."""
+    del stream
     if not contours_l or not contours_r:  # P/Main.cpp:405
         return []
-    s = contour_pair_scores(contour_descriptors(contours_l, device, stream),
-                            contour_descriptors(contours_r, device, stream), stream).cpu().numpy()
-    ii, jj = np.nonzero(s < 0.75)  # row-major: i-major, j-minor
-    return [(int(i), int(j), float(s[i, j])) for i, j in zip(ii, jj)]
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    n = max(len(contours_l), len(contours_r))
+    p = max(sum(len(c) for c in contours_l), sum(len(c) for c in contours_r))
+    m = _MATCHERS.get(idx)
+    if m is None or not m.fits(n, n, p, p):
+        with torch.cuda.device(idx):
+            m = ContourMatcherGPU(max(512, n), max(1 << 16, p))
+        _MATCHERS[idx] = m
+    return m(contours_l, contours_r)

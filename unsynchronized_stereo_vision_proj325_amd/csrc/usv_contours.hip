@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "usv.h"
 
@@ -132,8 +133,66 @@ __global__ void __launch_bounds__(256) pair_score_kernel(const double* __restric
 
 usv_status status_of(hipError_t e) { return e == hipSuccess ? USV_OK : USV_ERR_HIP; }
 
+// GenerateMatchingList's whole selection on the device: one wave per row i of the score matrix walks
+// j in chunks of 64 lanes, keeps v < 0.75 (NaN fails the test, as in the reference's `if`), and
+// compacts the survivors of each chunk in lane order with a ballot + mbcnt, so row i's matches land at
+// out + i * n_b in j order; counts[i] gets the row's count.  i-major, j-minor: the host concatenates
+// the rows in order (P/Main.cpp:408-420).
+__global__ void __launch_bounds__(256) match_select_kernel(const double* __restrict__ da, int n_a,
+                                                           const double* __restrict__ db, int n_b,
+                                                           usv_match* __restrict__ out, int* __restrict__ counts) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n_a) return;
+    double a[kDesc];
+#pragma unroll
+    for (int k = 0; k < kDesc; ++k) a[k] = da[(size_t)i * kDesc + k];
+    usv_match* row = out + (size_t)i * n_b;
+    int n = 0;
+    for (int j0 = 0; j0 < n_b; j0 += 64) {
+        const int j = j0 + lane;
+        bool keep = false;
+        double v = 0;
+        if (j < n_b) {
+            const double* b = db + (size_t)j * kDesc;
+            for (int k = 0; k < 7; ++k) {
+                const double ma = a[k], mb = b[k];
+                if (!__builtin_isnan(ma) && !__builtin_isnan(mb)) v += fabs(-ma + mb);
+            }
+            v += fabs((a[7] - b[7]) / ((a[7] + b[7]) / 2));
+            keep = v < 0.75;
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const int slot = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            row[slot].left_index = (unsigned)i;
+            row[slot].right_index = (unsigned)j;
+            row[slot].match_value = v;
+        }
+        n += __popcll(m);
+    }
+    if (lane == 0) counts[i] = n;
+}
+
 }  // namespace
 }  // namespace usv
+
+// Device matcher object: pinned host staging for the two contour sets and the results, device buffers
+// sized for max_contours per set and max_points per set, one stream.  One call = one H2D copy of both
+// sets, the descriptor launch (both sets), the select launch, one D2H of counts + padded rows, and a
+// host concatenation of the rows in order.
+struct usv_contour_matcher {
+    int max_n = 0, max_pts = 0, device = 0;
+    hipStream_t stream = nullptr;
+    // host pinned block: off_a[max_n + 1] off_b[max_n + 1] pts_a[2 max_pts] pts_b[2 max_pts] (ints)
+    int* h_in = nullptr;
+    int* d_in = nullptr;
+    double* d_desc = nullptr;   // 2 max_n x kDesc
+    usv_match* d_rows = nullptr;  // max_n x max_n
+    int* d_counts = nullptr;      // max_n (followed in the same allocation by nothing else)
+    usv_match* h_rows = nullptr;  // pinned copy of d_rows
+    int* h_counts = nullptr;      // pinned
+};
 
 extern "C" {
 
@@ -154,6 +213,117 @@ usv_status usv_contour_pair_scores(const double* desc_a, int n_a, const double* 
     hipLaunchKernelGGL(usv::pair_score_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), desc_a, n_a, desc_b, n_b, scores);
     return usv::status_of(hipGetLastError());
+}
+
+usv_status usv_contour_matcher_create(int max_contours, int max_points, usv_contour_matcher** out) {
+    if (!out) return USV_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (max_contours < 1 || max_points < 1 || max_contours > 16384) return USV_ERR_INVALID_ARG;
+    auto* m = new usv_contour_matcher;
+    m->max_n = max_contours;
+    m->max_pts = max_points;
+    const size_t n_in = 2 * ((size_t)max_contours + 1) + 4 * (size_t)max_points;
+    const size_t rows = (size_t)max_contours * max_contours;
+    bool ok = hipGetDevice(&m->device) == hipSuccess &&
+              hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc(&m->h_in, n_in * sizeof(int), hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&m->d_in, n_in * sizeof(int)) == hipSuccess &&
+              hipMalloc(&m->d_desc, 2 * (size_t)max_contours * usv::kDesc * sizeof(double)) == hipSuccess &&
+              hipMalloc(&m->d_rows, rows * sizeof(usv_match)) == hipSuccess &&
+              hipMalloc(&m->d_counts, (size_t)max_contours * sizeof(int)) == hipSuccess &&
+              hipHostMalloc(&m->h_rows, rows * sizeof(usv_match), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&m->h_counts, (size_t)max_contours * sizeof(int), hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
+        usv_contour_matcher_destroy(m);
+        return USV_ERR_HIP;
+    }
+    *out = m;
+    return USV_OK;
+}
+
+usv_status usv_contour_matcher_destroy(usv_contour_matcher* m) {
+    if (!m) return USV_ERR_INVALID_ARG;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    (void)hipHostFree(m->h_in);
+    (void)hipFree(m->d_in);
+    (void)hipFree(m->d_desc);
+    (void)hipFree(m->d_rows);
+    (void)hipFree(m->d_counts);
+    (void)hipHostFree(m->h_rows);
+    (void)hipHostFree(m->h_counts);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    (void)hipSetDevice(cur);
+    delete m;
+    return USV_OK;
+}
+
+usv_status usv_generate_matching_list_gpu(usv_contour_matcher* m, const int* pts_a, const int* off_a, int n_a,
+                                          const int* pts_b, const int* off_b, int n_b, usv_match* out, int cap,
+                                          int* n_out) {
+    if (!m || !n_out || n_a < 0 || n_b < 0 || cap < 0 || (cap && !out)) return USV_ERR_INVALID_ARG;
+    *n_out = 0;
+    if (n_a == 0 || n_b == 0) return USV_OK;  // P/Main.cpp:405: an empty set matches nothing
+    if (!pts_a || !off_a || !pts_b || !off_b) return USV_ERR_INVALID_ARG;
+    if (n_a > m->max_n || n_b > m->max_n) return USV_ERR_UNSUPPORTED;
+    const int pa = off_a[n_a], pb = off_b[n_b];
+    if (off_a[0] != 0 || off_b[0] != 0 || pa < 0 || pb < 0 || pa > m->max_pts || pb > m->max_pts)
+        return USV_ERR_INVALID_ARG;
+    for (int i = 0; i < n_a; ++i)
+        if (off_a[i + 1] < off_a[i]) return USV_ERR_INVALID_ARG;
+    for (int i = 0; i < n_b; ++i)
+        if (off_b[i + 1] < off_b[i]) return USV_ERR_INVALID_ARG;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(m->device) != hipSuccess) return USV_ERR_HIP;
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{cur};
+    // one contiguous block: off_a | off_b | pts_a | pts_b
+    int* h = m->h_in;
+    std::memcpy(h, off_a, (size_t)(n_a + 1) * sizeof(int));
+    std::memcpy(h + n_a + 1, off_b, (size_t)(n_b + 1) * sizeof(int));
+    std::memcpy(h + n_a + n_b + 2, pts_a, 2 * (size_t)pa * sizeof(int));
+    std::memcpy(h + n_a + n_b + 2 + 2 * (size_t)pa, pts_b, 2 * (size_t)pb * sizeof(int));
+    const size_t n_in = (size_t)n_a + n_b + 2 + 2 * ((size_t)pa + pb);
+    hipStream_t s = m->stream;
+    const int* d_off_a = m->d_in;
+    const int* d_off_b = m->d_in + n_a + 1;
+    const int* d_pts_a = m->d_in + n_a + n_b + 2;
+    const int* d_pts_b = d_pts_a + 2 * (size_t)pa;
+    double* desc_a = m->d_desc;
+    double* desc_b = m->d_desc + (size_t)m->max_n * usv::kDesc;
+    auto fail = [&](usv_status st) {
+        (void)hipStreamSynchronize(s);
+        return st;
+    };
+    if (hipMemcpyAsync(m->d_in, h, n_in * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) return fail(USV_ERR_HIP);
+    hipLaunchKernelGGL(usv::contour_desc_kernel, dim3((unsigned)((n_a + 63) / 64)), dim3(64), 0, s, d_pts_a, d_off_a, n_a,
+                       desc_a);
+    hipLaunchKernelGGL(usv::contour_desc_kernel, dim3((unsigned)((n_b + 63) / 64)), dim3(64), 0, s, d_pts_b, d_off_b, n_b,
+                       desc_b);
+    hipLaunchKernelGGL(usv::match_select_kernel, dim3((unsigned)((n_a + 3) / 4)), dim3(256), 0, s, desc_a, n_a, desc_b,
+                       n_b, m->d_rows, m->d_counts);
+    if (hipGetLastError() != hipSuccess) return fail(USV_ERR_HIP);
+    // rows are n_b apart on the device: copy the n_a x n_b block (packed by construction) and the counts
+    if (hipMemcpyAsync(m->h_counts, m->d_counts, (size_t)n_a * sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(m->h_rows, m->d_rows, (size_t)n_a * n_b * sizeof(usv_match), hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+        return fail(USV_ERR_HIP);
+    if (hipStreamSynchronize(s) != hipSuccess) return USV_ERR_HIP;
+    long long total = 0;
+    for (int i = 0; i < n_a; ++i) total += m->h_counts[i];
+    if (total > cap) return USV_ERR_INVALID_ARG;  // as usv_generate_matching_list: out must hold every match
+    int at = 0;
+    for (int i = 0; i < n_a; ++i) {
+        const int c = m->h_counts[i];
+        if (c > 0) std::memcpy(out + at, m->h_rows + (size_t)i * n_b, (size_t)c * sizeof(usv_match));
+        at += c;
+    }
+    *n_out = at;
+    return USV_OK;
 }
 
 }  // extern "C"

@@ -24,7 +24,7 @@
     defined(USV_GROUP_OCC) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
     defined(USV_GROUP_WEIGHTS) || defined(USV_PREP_THREADS) || defined(USV_HSV_PK) || defined(USV_PREP_KU) ||    \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
-    defined(USV_REMAP_LDS)
+    defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD)
 #error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
 #endif
 #define USV_BUILD_KIND "product build"

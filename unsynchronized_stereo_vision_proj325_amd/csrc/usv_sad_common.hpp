@@ -350,10 +350,17 @@ __device__ __forceinline__ void lds_barrier() {
 // prologue: vector-memory ops retire in order, so the first row's counted DMA wait also retires them, and
 // nothing waits on the table's own round trip (a register load + ds_write + barrier waited vmcnt(0)).
 // Every wave of a workgroup stages the whole table (identical bytes): no barrier before its first use.
+// N = 1: the first 128 entries only (a kernel whose disparities are all < 128: 1 KB less LDS).
+template <int N = 2>
 __device__ __forceinline__ void lut_dma(const double* lut, uint32_t* lds, int lane) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2\n\t"
-                 "global_load_lds_dwordx4 %0, %2 offset:1024"
-                 :: "v"((uint32_t)lane * 16u), "s"(lds_addr(lds)), "s"(lut) : "memory", "m0");
+    static_assert(N == 1 || N == 2, "one or two 1 KB halves");
+    if constexpr (N == 2)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2\n\t"
+                     "global_load_lds_dwordx4 %0, %2 offset:1024"
+                     :: "v"((uint32_t)lane * 16u), "s"(lds_addr(lds)), "s"(lut) : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2"
+                     :: "v"((uint32_t)lane * 16u), "s"(lds_addr(lds)), "s"(lut) : "memory", "m0");
 }
 
 // Scalar-load an exact number of dwords (5, 6 or 8: never past the row) into SGPRs.
@@ -446,6 +453,40 @@ __device__ __forceinline__ void dma_row_buf(su4 rsrc, uint32_t soff, const uint3
                      "buffer_load_ubyte %4, %6, %7 offen offset:1024 lds"
                      :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "s"(m0), "s"(rsrc), "s"(soff)
                      : "memory", "m0");
+}
+// dma_row_buf with the LDS destination at a compile-time offset from an SGPR base: M0 = base + OFF in
+// one s_add (the static row ring's slot offsets are constants).
+template <int NQ, uint32_t OFF>
+__device__ __forceinline__ void dma_row_buf_at(su4 rsrc, uint32_t soff, const uint32_t (&vo)[NQ], uint32_t base) {
+    static_assert(NQ >= 1 && NQ <= 5, "1..5 DMAs per row");
+    if constexpr (NQ == 1)
+        asm volatile("s_add_u32 m0, %1, %4\n\ts_nop 0\n\tbuffer_load_ubyte %0, %2, %3 offen lds"
+                     :: "v"(vo[0]), "s"(base), "s"(rsrc), "s"(soff), "n"(OFF) : "memory", "m0", "scc");
+    else if constexpr (NQ == 2)
+        asm volatile("s_add_u32 m0, %2, %5\n\ts_nop 0\n\tbuffer_load_ubyte %0, %3, %4 offen lds\n\t"
+                     "buffer_load_ubyte %1, %3, %4 offen offset:256 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "s"(base), "s"(rsrc), "s"(soff), "n"(OFF) : "memory", "m0", "scc");
+    else if constexpr (NQ == 3)
+        asm volatile("s_add_u32 m0, %3, %6\n\ts_nop 0\n\tbuffer_load_ubyte %0, %4, %5 offen lds\n\t"
+                     "buffer_load_ubyte %1, %4, %5 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %4, %5 offen offset:512 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(base), "s"(rsrc), "s"(soff), "n"(OFF)
+                     : "memory", "m0", "scc");
+    else if constexpr (NQ == 4)
+        asm volatile("s_add_u32 m0, %4, %7\n\ts_nop 0\n\tbuffer_load_ubyte %0, %5, %6 offen lds\n\t"
+                     "buffer_load_ubyte %1, %5, %6 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %5, %6 offen offset:512 lds\n\t"
+                     "buffer_load_ubyte %3, %5, %6 offen offset:768 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(base), "s"(rsrc), "s"(soff), "n"(OFF)
+                     : "memory", "m0", "scc");
+    else
+        asm volatile("s_add_u32 m0, %5, %8\n\ts_nop 0\n\tbuffer_load_ubyte %0, %6, %7 offen lds\n\t"
+                     "buffer_load_ubyte %1, %6, %7 offen offset:256 lds\n\t"
+                     "buffer_load_ubyte %2, %6, %7 offen offset:512 lds\n\t"
+                     "buffer_load_ubyte %3, %6, %7 offen offset:768 lds\n\t"
+                     "buffer_load_ubyte %4, %6, %7 offen offset:1024 lds"
+                     :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "s"(base), "s"(rsrc), "s"(soff),
+                        "n"(OFF) : "memory", "m0", "scc");
 }
 template <int N>
 __device__ __forceinline__ typename SWords<N>::T s_load_words_off(const uint8_t* p, uint32_t off) {

@@ -4,6 +4,11 @@
 // Spec: SURVEY.md §8(a) A1 (restated in oracle/sad_oracle.c); DESIGN.md §3 has the derivation.  The
 // reference has no block matcher; its nearest primitive is the u8 absdiff motion mask
 // at P/Main.cpp:304.  Integer arithmetic only: bit-exact with the oracle by construction.
+#include <array>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "usv_sad_common.hpp"
 
 namespace usv {
@@ -24,20 +29,13 @@ namespace {
 // 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
 // rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
 // ===================================================================================
-#ifndef USV_PAIR_PIPE
-#define USV_PAIR_PIPE 1  // argmin transpose of row t finished during row t + 1 (latency hidden by the chain)
-#endif
-#ifndef USV_NT_DIST
-#define USV_NT_DIST 0  // experiment: the paired kernel's distance map through non-temporal stores
-#endif
 #ifndef USV_WIDE_FLUSH
 #define USV_WIDE_FLUSH 1  // paired kernel: one 8-byte disparity store and one 16-byte distance store per lane per chunk
 #endif
-#ifndef USV_PAIR_PIPE_R7
-#define USV_PAIR_PIPE_R7 0  // experiment: pipelined argmin at r = 7 (needs USV_PAIR_OCC7=2, USV_PAIR_SPLIT_R=8)
-#endif
+// Argmin transpose of row t finished during row t + 1 (latency hidden by the chain): r = 5 only (at
+// r = 6, 7 the held transpose words spill).
 template <int RAD>
-constexpr bool kPairPipe = USV_PAIR_PIPE && (RAD == 5 || (RAD == 7 && USV_PAIR_PIPE_R7));
+constexpr bool kPairPipe = RAD == 5;
 template <int RAD, int NW>
 struct PCfg {
     static constexpr int K = 8;
@@ -49,19 +47,41 @@ struct PCfg {
     static constexpr int NR = 2 * 63 + NE_V;            // entries a wave stages per row
     static constexpr int NQ = (NR + 63) / 64;           // DMA instructions per row
     static constexpr int NRS = NQ * 64;
-    static constexpr int NB = 8;                        // ring slots per wave
+    // Ring slots per wave.  r = 5 with one wave: WIN slots (a static ring -- row t sits in slot t mod WIN,
+    // so in the WIN-unrolled row loop every slot, LDS offset and M0 value is a compile-time constant;
+    // 12 waves x 13.0 KB fit the CU's 160 KB).  Otherwise 8 slots indexed t & 7 (r = 6, 7 or two waves
+    // per workgroup would not fit WIN slots at three waves per SIMD).
+#ifndef USV_PAIR_STATIC
+#define USV_PAIR_STATIC 1
+#endif
+#ifndef USV_PAIR_PD
+#define USV_PAIR_PD 0  // rows of DMA look-ahead (0: NB - 1)
+#endif
+    static constexpr bool STATIC = USV_PAIR_STATIC && RAD == 5 && NW == 1;
+    static constexpr int NB = STATIC ? WIN : 8;
 #ifndef USV_PAIR_SPLIT_R
 #define USV_PAIR_SPLIT_R 7  // radius from which the row's entries are read in two batches
 #endif
     static constexpr int SPLIT = RAD >= USV_PAIR_SPLIT_R ? 2 : 1;
-    static constexpr int PD = NB - 1;
+    static constexpr int PD = USV_PAIR_PD > 0 && USV_PAIR_PD < NB ? USV_PAIR_PD : NB - 1;
     static constexpr int KRB = WIN;
     static constexpr int RBUF_OFF = 0;
     static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
     static constexpr int TB_WORDS = K * 64;
     static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
-    static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
-    static constexpr int SMEM_WORDS = LUT_OFF + 2 * 256;
+    // one wave: its LDS ops run in order, so the flush's reads of a chunk precede the next chunk's
+    // writes and one combine buffer suffices (slot addresses are then compile-time); two or more waves
+    // alternate two buffers so a flush needs one barrier
+    static constexpr int NCB = NW == 1 ? 1 : 2;
+    static constexpr int LUT_OFF = COMB_OFF + NCB * KRB * NW * K;
+#ifndef USV_PAIR_LDS_PAD
+#define USV_PAIR_LDS_PAD 0  // probe: extra LDS words per workgroup
+#endif
+    // distance table in LDS: one wave means D <= 128, so every output disparity is < 128 and half the
+    // table suffices (1 KB less: the static ring's 12 workgroups per CU fit only below ~12.5 KB each,
+    // profiles/probes_r04/lds_residency_r04.txt)
+    static constexpr int LUTN = NW == 1 ? 128 : 256;
+    static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN + USV_PAIR_LDS_PAD;
     static_assert(RAD >= 2 && RAD <= 7, "paired kernel: 5 <= w <= 15");
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
@@ -137,8 +157,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     for (int i = 0; i < C::NQ; ++i)
         colRb[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1) + kDmaBias - 256u * (uint32_t)i;
     const uint32_t rbase = lds_addr(rbuf);
-    auto issue_dma = [&](int t) {
-        const int buf = t & (NB - 1);
+    // ring slot of input row t (static ring: t mod WIN, known at compile time wherever it is used)
+    auto slot_of = [&](int t) { return C::STATIC ? t % NB : (t & (NB - 1)); };
+    auto issue_dma = [&](int t, int buf) {
         dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
     };
     LWords lw_next;
@@ -151,13 +172,20 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * NDMA>();
         __builtin_amdgcn_wave_barrier();
+        // static ring: rows of an unrolled group sit at t = (multiple of WIN) + I, so row t + PD's slot is
+        // (I + PD) mod WIN
+        constexpr int SLOT_NEXT = C::STATIC ? (I + PD) % NB : -1;
         if constexpr (WARM) {
-            issue_dma(t + PD);
+            issue_dma(t + PD, C::STATIC ? SLOT_NEXT : slot_of(t + PD));
         } else {
             int rr = rawR;
             asm volatile("" : "+s"(rr));
-            const int buf = (t + PD) & (NB - 1);
-            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            if constexpr (C::STATIC) {
+                dma_row_buf_at<C::NQ, 4u * SLOT_NEXT * C::NRS>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase);
+            } else {
+                const int buf = slot_of(t + PD);
+                dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+            }
             rawR = rr + a.pitch;
         }
         // (pipelined argmin: the ring row leaving the window is subtracted first, so its registers
@@ -182,8 +210,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         }
         auto lbyte = [&](int j) -> uint32_t { return Lv[j]; };
         using VT = typename VecT<C::VEC>::T;
-        int boff = (t & (NB - 1)) * C::NRS;
-        asm volatile("" : "+s"(boff));
+        int boff = C::STATIC ? I * C::NRS : slot_of(t) * C::NRS;
+        if constexpr (!C::STATIC) asm volatile("" : "+s"(boff));
         const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
         // The staged entries come in C::SPLIT batches of vector reads, each consumed by the chain
         // steps it completes before the next batch is read (r = 7: fewer live VGPRs, so three
@@ -257,7 +285,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         asm volatile("" : "+v"(tid));
         if (wide) {
             static_assert(K == 8, "one 8-byte disparity store per row");
-            const uint32_t* crow = comb + (cb * KRB) * NW * K;
+            const uint32_t* crow = comb + (C::NCB > 1 ? cb * KRB * NW * K : 0);
             if (tid < rows) {
                 uint4 k0 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[0];
                 uint4 k1 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[1];
@@ -284,16 +312,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                     kk = make_uint2(min(kk.x, m.x), min(kk.y, m.y));
                 }
                 const size_t y = (size_t)(y_chunk + r);
-                if constexpr (USV_NT_DIST) {  // experiment: write-once map as non-temporal stores
-                        typedef double v2d __attribute__((ext_vector_type(2)));
-                        v2d v = {lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
-                        __builtin_nontemporal_store(v, reinterpret_cast<v2d*>(dist + y * a.dist_pitch + x0 + 2 * q));
-                    } else {
-                        *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
-                    }
+                *reinterpret_cast<D2*>(dist + y * a.dist_pitch + x0 + 2 * q) = D2{lut_s[kk.x & 0xFFu], lut_s[kk.y & 0xFFu]};
             }
             y_chunk += rows;
-            cb ^= 1;
+            if constexpr (C::NCB > 1) cb ^= 1;
             return;
         }
         const int items = rows * K;
@@ -301,14 +323,14 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             const int row = i / K, p = i - row * K;
             uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((cb * KRB + row) * NW + w2) * K + p]);
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[(((C::NCB > 1 ? cb : 0) * KRB + row) * NW + w2) * K + p]);
             const uint32_t dv = key & 0xFFu;
             const size_t y = (size_t)(y_chunk + row);
             disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
             if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
         }
         y_chunk += rows;
-        cb ^= 1;
+        if constexpr (C::NCB > 1) cb ^= 1;
     };
     // Argmin of one row, in two halves so that the LDS round trip of the transpose and the
     // dependent min / DPP tail overlap the next row's chain (USV_PAIR_PIPE):
@@ -370,7 +392,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 asm volatile("" : "+v"(px));
                 px = (px & 63) >> 3;
             }
-            comb[((cb * KRB + slot) * NW + wave) * K + px] = fm;
+            comb[(((C::NCB > 1 ? cb : 0) * KRB + slot) * NW + wave) * K + px] = fm;
         }
     };
     auto tr_finish = [&](int slot) {
@@ -385,136 +407,13 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     };
     auto no_pre = [](auto) {};
 
-    // ---- prefetched row boundary (USV_PAIR_PREF, pipelined r = 5 only) ----
-    // Without it every row starts with an s_waitcnt lgkmcnt(0) (the pinned L words are a scalar
-    // load, which returns out of order) that also retires the previous row's transpose reads issued
-    // just before, then issues its staged-entry reads and waits for the first of them: two LDS round
-    // trips per row with nothing else of this wave to issue.  Here the boundary is reordered:
-    //   end of row t:  lgkmcnt(0) (everything of row t, and the L words of row t + 1 loaded a row
-    //                  earlier) -> extract row t + 1's L bytes -> [flush] -> scalar-load row t + 2's
-    //                  L words -> vmcnt wait for row t + 1's DMA -> the first PV vector reads of
-    //                  row t + 1's staged entries -> row t's transpose WRITES;
-    //   row t + 1:     DMA, ring subtraction, the remaining entry reads, THEN the transpose reads,
-    //                  the chain (its first steps run on the prefetched entries) with the argmin
-    //                  pieces from step PIECE_OFF on, so the transpose reads have a whole run of
-    //                  chain steps to land.
-#ifndef USV_PAIR_PREF
-#define USV_PAIR_PREF 0  // vector reads of the next row prefetched (0 = off)
-#endif
-#ifndef USV_PAIR_PIECE_OFF
-#define USV_PAIR_PIECE_OFF 8  // chain step of the first argmin piece (USV_PAIR_PREF)
-#endif
-    constexpr bool PREF = USV_PAIR_PREF > 0 && kPairPipe<RAD> && C::SPLIT == 1;
-    using VTp = typename VecT<C::VEC>::T;
-    constexpr int NVp = C::NE_V / C::VEC;
-    constexpr int PV = PREF ? (USV_PAIR_PREF < NVp ? USV_PAIR_PREF : NVp) : 1;
-    constexpr int OFFP = USV_PAIR_PIECE_OFF;
-    uint32_t Epf[PV * C::VEC];
-    uint32_t Lv[NPOS];  // L bytes of the row about to run
-    auto extract_l = [&]() {  // after wait_lgkm0_pin(lw_next)
-        LWords cur = lw_next;
-        uint32_t lw[8];
-        unpack_words<LS::NLD>(cur, lw);
-#pragma unroll
-        for (int j = 0; j < NPOS; ++j) {
-            const int bidx = LS::byte(j);
-            if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
-            else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
-        }
-    };
-    auto prefetch_e = [&](int t_next) {
-        wait_vmcnt<(PD - 1) * NDMA>();  // row t_next's DMA (issued PD rows ago) has landed
-        __builtin_amdgcn_wave_barrier();
-        int boff = (t_next & (NB - 1)) * C::NRS;
-        asm volatile("" : "+s"(boff));
-        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
-#pragma unroll
-        for (int k = 0; k < PV; ++k) {
-            const VTp v = rb[k];
-#pragma unroll
-            for (int e = 0; e < C::VEC; ++e) Epf[k * C::VEC + e] = vget<C::VEC>(v, e);
-        }
-    };
-    auto tr_write = [&](const uint32_t(&S)[K]) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
-        asm volatile("" ::: "memory");
-    };
-    auto tr_read = [&]() {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) trq[j] = reinterpret_cast<const uint4*>(tb)[rdw[j]];
-        asm volatile("" ::: "memory");
-    };
-    auto do_row_pref = [&](int t_in, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
-        constexpr int I = decltype(i_tag)::value;
-        int t = t_in;
-        asm volatile("" : "+s"(t));
-        {
-            int rr = rawR;
-            asm volatile("" : "+s"(rr));
-            const int buf = (t + PD) & (NB - 1);
-            dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
-            rawR = rr + a.pitch;
-        }
-#pragma unroll
-        for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
-        uint32_t E[C::NE_V];
-#pragma unroll
-        for (int e = 0; e < PV * C::VEC; ++e) E[e] = Epf[e];
-        int boff = (t & (NB - 1)) * C::NRS;
-        asm volatile("" : "+s"(boff));
-        const VTp* rb = reinterpret_cast<const VTp*>(rbuf + boff + s_l);
-#pragma unroll
-        for (int k = PV; k < NVp; ++k) {
-            const VTp v = rb[k];
-#pragma unroll
-            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
-        }
-        tr_read();
-        uint32_t A[NPOS + 1];
-        A[0] = 0;
-        auto chain_step = [&](auto jt) {
-            constexpr int j = decltype(jt)::value;
-            const uint32_t l = Lv[j];
-            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
-            if constexpr (j >= OFFP && j - OFFP < 16) tr_piece(std::integral_constant<int, j - OFFP>{}, I);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        [&]<int... J>(std::integer_sequence<int, J...>) {
-            (chain_step(std::integral_constant<int, J>{}), ...);
-        }(std::make_integer_sequence<int, NPOS>{});
-        [&]<int... J>(std::integer_sequence<int, J...>) {
-            ((J >= (NPOS - OFFP > 0 ? NPOS - OFFP : 0) ? tr_piece(std::integral_constant<int, J>{}, I) : void()), ...);
-        }(std::make_integer_sequence<int, 16>{});
-#pragma unroll
-        for (int x = 0; x < K; ++x) {
-            const uint32_t h = A[x + WIN] - A[x];
-            S[x] = S[x] + h;
-            ring[I][x] = h;
-        }
-    };
-    auto row_tail = [&](int t, bool do_flush, const uint32_t(&S)[K]) {
-        wait_lgkm0_pin<LS::NLD>(lw_next);
-        extract_l();
-        if (do_flush) flush(KRB);
-        {
-            int rl = rawL;
-            asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
-            rawL = rl + a.pitch;
-        }
-        prefetch_e(t + 1);
-        tr_write(S);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
     uint32_t S[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) S[i] = 0;
     uint32_t ring[WIN][K];
     static_assert(C::LUT_OFF % 4 == 0, "16-byte aligned table");
-    if (dist) lut_dma(a.lut, smem + C::LUT_OFF, lane);
-    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P), ...); }(std::make_integer_sequence<int, PD>{});
+    if (dist) lut_dma<C::LUTN / 128>(a.lut, smem + C::LUT_OFF, lane);
+    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P, P % NB), ...); }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
     using WarmT = std::integral_constant<bool, true>;
     using SteadyT = std::integral_constant<bool, false>;
@@ -528,9 +427,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     constexpr bool PIPE = kPairPipe<RAD>;
     static_assert(KRB == WIN, "pending slot = row index in the unrolled group");
     static_assert(!PIPE || NPOS >= 16, "16 argmin pieces ride on the chain steps");
-    if constexpr (PREF) {
-        row_tail(WIN - 1, false, S);
-    } else if constexpr (PIPE) {
+    if constexpr (PIPE) {
         tr_issue(S);
         __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -538,10 +435,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     }
     auto step = [&](int t0, auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
-        if constexpr (PREF) {
-            do_row_pref(t0 + I, i_tag, S, ring);
-            row_tail(t0 + I, I == KRB - 1, S);
-        } else if constexpr (PIPE) {
+        if constexpr (PIPE) {
             do_row(t0 + I, SteadyT{}, i_tag, S, ring, [&](auto jt) {
                 if constexpr (decltype(jt)::value < 16) tr_piece(jt, I);
             });
@@ -554,7 +448,17 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
         }
     };
-    for (int t0 = WIN; t0 < T; t0 += WIN) {
+    int t0 = WIN;
+    if constexpr (EDGE == kInterior && C::STATIC) {
+        // whole groups without a bound check per row (r = 5 interior tiles: the edge tiles keep one copy
+        // of the row code; at r = 6, 7 the unchecked copy spills)
+        for (; t0 + WIN <= T; t0 += WIN) {
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                (step(t0, std::integral_constant<int, I>{}), ...);
+            }(std::make_integer_sequence<int, WIN>{});
+        }
+    }
+    for (; t0 < T; t0 += WIN) {
         [&]<int... I>(std::integer_sequence<int, I...>) {
             bool go = true;
             ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
@@ -563,7 +467,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load before its SGPRs are reused
     if constexpr (PIPE) {
         const int last = (nout - 1) % KRB;  // the pending slot: the band's last output row
-        if constexpr (PREF) tr_read();
         tr_finish(last);
         if (last == KRB - 1) flush(KRB);
     }
@@ -580,19 +483,17 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #endif
 constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : USV_PAIR_OCC5; }
 
-template <int RAD, int NW>
-__global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
-                                                              const uint8_t* __restrict__ R,
-                                                              uint8_t* __restrict__ disp,
-                                                              double* __restrict__ dist, MatchArgs a, BandPlan P) {
-    using C = PCfg<RAD, NW>;
-    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // the work map of sad_fast_kernel (XCD-contiguous tile runs, generation-weighted bands)
-    const unsigned total = gridDim.x, lin = blockIdx.x;
+// Work map of one launch (the sad_fast_kernel map: XCD-contiguous tile runs, generation-weighted
+// bands): workgroup `lin` of `total` -> its x-tile, pair and output rows.  Host and device run the
+// same function: the launcher tabulates it once per launch geometry (tile_table), so a workgroup
+// normally reads its span with one scalar load instead of ~500 SALU of divisions and band sums.
+struct TileSpan {
+    unsigned xt, pair;
+    int y_begin, y_end;
+};
+__host__ __device__ __forceinline__ TileSpan tile_span(unsigned lin, unsigned total, const BandPlan& P, int H) {
     const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
+    const unsigned tile = xcd * base + (xcd < rem ? xcd : rem) + (lin >> 3);
     const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
     const bool past = tile >= per_pair && P.extra > 0;
     const unsigned col_xt = past ? tile - per_pair : tile % nxt;
@@ -602,14 +503,40 @@ __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(co
     const unsigned long_run = base + 1u, split = rem * long_run;
     const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
                                   (unsigned)P.gen_g, P.weights);
-    const unsigned pre = bs.pre, tot = bs.tot;
-    const int xt = (int)col_xt;
+    return TileSpan{col_xt, pair, (int)((unsigned long long)H * bs.pre / bs.tot),
+                    (int)((unsigned long long)H * (bs.pre + bs.own) / bs.tot)};
+}
+
+template <int RAD, int NW>
+__global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
+                                                              const uint8_t* __restrict__ R,
+                                                              uint8_t* __restrict__ disp,
+                                                              double* __restrict__ dist, MatchArgs a, BandPlan P,
+                                                              const uint2* __restrict__ tiles) {
+    using C = PCfg<RAD, NW>;
+    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned xtu, pair;
+    int y_begin, y_end;
+    if (tiles) {  // the launcher's table: x-tile | pair << 16, y_begin | y_end << 16
+        const uint2 t = tiles[blockIdx.x];
+        xtu = t.x & 0xFFFFu;
+        pair = t.x >> 16;
+        y_begin = (int)(t.y & 0xFFFFu);
+        y_end = (int)(t.y >> 16);
+    } else {
+        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P, a.H);
+        xtu = sp.xt;
+        pair = sp.pair;
+        y_begin = sp.y_begin;
+        y_end = sp.y_end;
+    }
+    const int xt = (int)xtu;
     const int n_xt = P.n_xt;
     int x0 = xt * C::K;
     if (xt == n_xt - 1) x0 = a.W - C::K;
     else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * C::K);
-    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
@@ -656,6 +583,38 @@ int resident_pair_blocks_per_cu() {
 #define USV_PAIR_GEN_WEIGHTS_NW2 0x41415564u  // 100, 85, 65, 65
 #endif
 
+// The work map of a launch geometry as a device table (one uint2 per workgroup), built on the host
+// from tile_span and uploaded once (synchronously) per geometry and device; immutable afterwards, so
+// any stream may read it.  nullptr (the kernel computes its span itself) while the stream is being
+// captured into a graph and the geometry has no table yet, or when a field does not fit 16 bits.
+const uint2* tile_table(int rad, int nw, const MatchArgs& a, const BandPlan& P, unsigned total, hipStream_t s) {
+    if (a.H > 0xFFFF || P.n_xt > 0xFFFF || a.batch > 0xFFFF) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::array<long long, 11> key{dev, rad, nw, a.W, a.H, a.batch, P.n_xt, P.m, P.extra,
+                                        ((long long)P.gen_g << 32) | P.weights, total};
+    static std::mutex mu;
+    static std::map<std::array<long long, 11>, uint2*> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    std::vector<uint2> host(total);
+    for (unsigned lin = 0; lin < total; ++lin) {
+        const TileSpan sp = tile_span(lin, total, P, a.H);
+        host[lin] = make_uint2(sp.xt | (sp.pair << 16), (unsigned)sp.y_begin | ((unsigned)sp.y_end << 16));
+    }
+    uint2* d = nullptr;
+    if (hipMalloc(&d, total * sizeof(uint2)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, host.data(), total * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    cache.emplace(key, d);
+    return d;
+}
+
 template <int RAD, int NW>
 hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     constexpr int K = PCfg<RAD, NW>::K, WIN = 2 * RAD + 1;
@@ -684,7 +643,8 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
               : NW > 1 ? USV_PAIR_GEN_WEIGHTS_NW2
               : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
     dim3 grid((unsigned)total), block(NW * 64);
-    hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
+    const uint2* tiles = tile_table(RAD, NW, a, P, (unsigned)total, s);
+    hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P, tiles);
     return hipGetLastError();
 }
 
