@@ -8,7 +8,7 @@ ROUNDS=${ROUNDS:-3}
 ARGS=${ARGS:---steps 200 --warmup 20 --no-cpu-baseline --extra-steps 0}
 out=gpurun_out/ab.txt; : > $out
 for r in $(seq $ROUNDS); do
-  for v in default build_variants/*.so; do
+  for v in default ${VARIANTS_DIR:-build_variants}/*.so; do
     n=$(basename $v .so)
     if [ "$v" = default ]; then lib=""; else lib=$PWD/$v; fi
     res=$(USV_LIB_PATH=$lib timeout -k 10 120 python bench.py $ARGS 2>/dev/null | tail -1)

@@ -8,14 +8,14 @@ name=$1; shift
 SRC=${VARIANT_SRC:-usv_sad_fast}   # which kernel file the defines apply to
 C=unsynchronized_stereo_vision_proj325_amd/csrc
 make -s -C $C
-mkdir -p build_variants
+OUTD=${VARIANTS_DIR:-build_variants}; mkdir -p $OUTD
 # VARIANT_FILE: compile this file in place of $C/$SRC.hip (e.g. an older revision from git show)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -I$C -ffp-contract=off -DUSV_VARIANT_BUILD=1 "$@" \
-    -c ${VARIANT_FILE:-$C/$SRC.hip} -o build_variants/$name.var.o
+    -c ${VARIANT_FILE:-$C/$SRC.hip} -o $OUTD/$name.var.o
 # the C ABI object again with USV_VARIANT_BUILD: usv_version() of a variant says "variant build"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Iinclude -I$C -ffp-contract=off -DUSV_VARIANT_BUILD=1 \
-    -c $C/usv_capi.hip -o build_variants/$name.capi.o
+    -c $C/usv_capi.hip -o $OUTD/$name.capi.o
 objs=$(ls $C/build/*.o | grep -v "/$SRC.o" | grep -v "/usv_capi.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name.so build_variants/$name.var.o build_variants/$name.capi.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -f build_variants/$name.var.o build_variants/$name.capi.o
-echo built build_variants/$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUTD/$name.so $OUTD/$name.var.o $OUTD/$name.capi.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -f $OUTD/$name.var.o $OUTD/$name.capi.o
+echo built $OUTD/$name.so

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for v in default build_variants/*.so; do
+for v in default ${VARIANTS_DIR:-build_variants}/*.so; do
   n=$(basename $v .so); lib=""; [ "$v" != default ] && lib=$PWD/$v
   USV_LIB_PATH=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/pp_$n -o pp --output-format csv \
      -- python3 scripts/prof_pipeline.py > gpurun_out/pp_$n.log 2>&1 || { echo "FAILED $n"; exit 1; }

@@ -5,10 +5,14 @@
 // rectifies and pre-processes it and hands it on (P/Main.cpp:876-921,
 // 1238-1242).  A per-frame blocking call (copy in, match, copy out, sync)
 // serialises the PCIe transfers with the kernel.  This engine keeps `depth`
-// frames in flight instead: every slot owns pinned host staging, device
-// buffers and its own HIP stream, so frame k+1's H2D, frame k's match and
+// frames in flight instead: every slot owns pinned host staging and device
+// buffers; three streams carry the stages -- H2D copies, the match, D2H copies
+// -- ordered per frame by events, so frame k+1's H2D, frame k's match and
 // frame k-1's D2H run at once (the copy engines are separate from the CUs and
-// PCIe is full duplex).  Results are the u8 disparity maps by default: the
+// PCIe is full duplex).  (Round 3 gave every slot its own stream and measured
+// depth 3 ~20 % slower than depth 2 or 4 -- streams share the process's four
+// hardware queues, so the overlap depended on how the slots' streams landed on
+// them; one stream per stage makes the schedule the same at every depth.)  Results are the u8 disparity maps by default: the
 // per-pixel distance is a 256-entry table lookup of the disparity
 // (P/DistanceCalculator.cpp:84), expanded on the host only where a caller asks
 // for it (usv_distance_expand_host), so the link carries 1 B per pixel instead
@@ -29,12 +33,12 @@ struct usv_frame_stream {
         double* hDist = nullptr;                                 // pinned (USV_STREAM_DEVICE_DIST)
         uint8_t *dL = nullptr, *dR = nullptr, *dDisp = nullptr;  // device
         double* dDist = nullptr;
-        hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        hipEvent_t in = nullptr, matched = nullptr, done = nullptr;  // after the H2D, the match, the D2H
         long long ticket = -1;  // frame in this slot, -1 = free
         bool ready = false;     // its results were waited for
     };
     std::vector<Slot> slot;
+    hipStream_t s_in = nullptr, s_match = nullptr, s_out = nullptr;  // H2D copies, matcher, D2H copies
     long long next = 0;      // ticket of the next submit
     double* lut = nullptr;   // device distance table (USV_STREAM_DEVICE_DIST)
 };
@@ -50,18 +54,20 @@ void free_slot(usv_frame_stream::Slot& s) {
     (void)hipFree(s.dR);
     (void)hipFree(s.dDisp);
     (void)hipFree(s.dDist);
+    if (s.in) (void)hipEventDestroy(s.in);
+    if (s.matched) (void)hipEventDestroy(s.matched);
     if (s.done) (void)hipEventDestroy(s.done);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
 }
 
 void release(usv_frame_stream* e) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(e->device);
-    for (auto& s : e->slot) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
-        free_slot(s);
-    }
+    for (hipStream_t st : {e->s_in, e->s_match, e->s_out})
+        if (st) (void)hipStreamSynchronize(st);
+    for (auto& s : e->slot) free_slot(s);
+    for (hipStream_t st : {e->s_in, e->s_match, e->s_out})
+        if (st) (void)hipStreamDestroy(st);
     (void)hipFree(e->lut);
     (void)hipSetDevice(cur);
     delete e;
@@ -111,11 +117,18 @@ usv_status usv_frame_stream_create(int W, int H, int D, int w, int metric, int d
             hipMalloc(&s.dDisp, e->frame) != hipSuccess ||
             (dd && (hipHostMalloc(&s.hDist, e->frame * sizeof(double), hipHostMallocDefault) != hipSuccess ||
                     hipMalloc(&s.dDist, e->frame * sizeof(double)) != hipSuccess)) ||
-            hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.matched, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
             release(e);
             return USV_ERR_HIP;
         }
+    }
+    if (hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_match, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking) != hipSuccess) {
+        release(e);
+        return USV_ERR_HIP;
     }
     if (dd) {
         double lut[256];
@@ -162,26 +175,26 @@ usv_status usv_frame_stream_submit(usv_frame_stream* e, const uint8_t* L, const 
     };
     stage(L, s.hL);
     stage(R, s.hR);
-    if (hipMemcpyAsync(s.dL, s.hL, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
-        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
-        (void)hipStreamSynchronize(s.stream);  // a first copy that was enqueued may still read the staging
-        return USV_ERR_HIP;
-    }
+    // every error path drains the three streams: nothing of this frame may still read the staging
+    auto drain = [&](usv_status st) {
+        for (hipStream_t q : {e->s_in, e->s_match, e->s_out}) (void)hipStreamSynchronize(q);
+        return st;
+    };
+    if (hipMemcpyAsync(s.dL, s.hL, e->frame, hipMemcpyHostToDevice, e->s_in) != hipSuccess ||
+        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, e->s_in) != hipSuccess ||
+        hipEventRecord(s.in, e->s_in) != hipSuccess || hipStreamWaitEvent(e->s_match, s.in, 0) != hipSuccess)
+        return drain(USV_ERR_HIP);
     const bool dd = e->flags & USV_STREAM_DEVICE_DIST;
     usv_status st = usv_sad_disparity_ex(s.dL, s.dR, e->W, e->H, e->W, e->D, e->w, e->metric, s.dDisp, e->W,
                                          dd ? s.dDist : nullptr, e->W, dd ? e->lut : nullptr, USV_KERNEL_AUTO,
-                                         s.stream);
-    if (st != USV_OK) {
-        (void)hipStreamSynchronize(s.stream);  // nothing of this frame may still read the staging
-        return st;
-    }
-    if (hipMemcpyAsync(s.hDisp, s.dDisp, e->frame, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
-        (dd && hipMemcpyAsync(s.hDist, s.dDist, e->frame * sizeof(double), hipMemcpyDeviceToHost, s.stream) !=
+                                         e->s_match);
+    if (st != USV_OK) return drain(st);
+    if (hipEventRecord(s.matched, e->s_match) != hipSuccess || hipStreamWaitEvent(e->s_out, s.matched, 0) != hipSuccess ||
+        hipMemcpyAsync(s.hDisp, s.dDisp, e->frame, hipMemcpyDeviceToHost, e->s_out) != hipSuccess ||
+        (dd && hipMemcpyAsync(s.hDist, s.dDist, e->frame * sizeof(double), hipMemcpyDeviceToHost, e->s_out) !=
                    hipSuccess) ||
-        hipEventRecord(s.done, s.stream) != hipSuccess) {
-        (void)hipStreamSynchronize(s.stream);
-        return USV_ERR_HIP;
-    }
+        hipEventRecord(s.done, e->s_out) != hipSuccess)
+        return drain(USV_ERR_HIP);
     s.ticket = e->next++;
     s.ready = false;
     *ticket = s.ticket;
