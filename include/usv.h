@@ -393,6 +393,20 @@ usv_status usv_rectify_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, 
                                       int cn, const uint32_t* pmapL, const uint32_t* pmapR, int W, int H,
                                       uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
 
+/* LDS-tiled form of the packed remap: 64 x 16 output tiles, each tile's source box (precomputed once
+ * per packed map by usv_remap_tile_boxes: 2 u32 per tile, ceil(W / 64) * ceil(H / 16) tiles, for
+ * `cn` channels) staged in LDS by coalesced loads together with the map; pixels whose taps leave the
+ * box take per-tap reads.  Bit-identical to usv_remap_packed_u8 / usv_rectify_pair_packed_u8; the
+ * packed map must be 16-byte aligned. */
+usv_status usv_remap_tile_boxes(const uint32_t* pmap, int W, int H, int sW, int sH, int cn, uint32_t* boxes,
+                                void* stream);
+usv_status usv_remap_packed_tiled_u8(const uint8_t* src, int sW, int sH, int spitch, int cn, const uint32_t* pmap,
+                                     const uint32_t* boxes, int W, int H, uint8_t* dst, int dpitch, void* stream);
+usv_status usv_rectify_pair_packed_tiled_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                            int cn, const uint32_t* pmapL, const uint32_t* pmapR,
+                                            const uint32_t* boxesL, const uint32_t* boxesR, int W, int H,
+                                            uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream);
+
 /* ---- calibration file: LoadCalibrationData, P/Main.cpp:329-349 ---- */
 
 /* A small dense matrix, row-major doubles (rows = cols = 0: empty, as an unread cv::Mat). */

@@ -12,7 +12,7 @@ step() {  # step <name> <cmd...>
   return 0
 }
 [ "${SKIP_PROBE:-0}" = 1 ] || step traffic bash scripts/gpu_traffic_probe.sh
-step tests timeout -k 10 300 python -u -m pytest tests/test_gpu_contours.py tests/test_streaming.py tests/test_sharded_engine.py \
+step tests timeout -k 10 400 python -u -m pytest tests/test_gpu_contours.py tests/test_streaming.py tests/test_sharded_engine.py tests/test_rectify.py \
     -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
 step pair_ab env ROUNDS=${ROUNDS:-3} bash scripts/gpu_ab_pair.sh
 if ls build_variants_pp/*.so > /dev/null 2>&1; then

@@ -15,6 +15,8 @@ W, H = 1920, 1080
 rng = np.random.default_rng(0)
 cl, cr = synthetic_calibration(W, H, seed=1)
 rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
+# the direct (untiled) packed remap beside the tiled default: both kernels in the same trace
+dl, dr = Rectifier(*cl, (W, H), device=dev, tiled=False), Rectifier(*cr, (W, H), device=dev, tiled=False)
 src = [torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev) for _ in range(2)]
 prep = FramePrep(dev)
 gray = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
@@ -22,6 +24,7 @@ prev = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
 pair = FramePrepPair(dev)
 for _ in range(int(os.environ.get("PP_ITERS", "20"))):
     ol, orr = rectify_pair(rl, rr, src[0], src[1])
+    rectify_pair(dl, dr, src[0], src[1])
     hsv, bgr, g = prep(ol)
     m, _ = ABSDiffSearch(gray, prev)
     pair(ol, orr)

@@ -130,6 +130,12 @@ SIGNATURES = {
     "usv_remap_pack_map": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "usv_remap_packed_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
                                     c_void_p]),
+    "usv_remap_tile_boxes": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "usv_remap_packed_tiled_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                          c_void_p, c_int, c_void_p]),
+    "usv_rectify_pair_packed_tiled_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                                                 c_void_p]),
     "usv_rectify_pair_packed_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "usv_rectify_prep_pair_packed_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,

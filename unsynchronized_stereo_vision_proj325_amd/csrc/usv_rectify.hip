@@ -152,6 +152,179 @@ __global__ __launch_bounds__(256) void pack_map_kernel(const int16_t* __restrict
     pmap[i] = pack_map_word(map1[2 * i], map1[2 * i + 1], map2[i], sW, sH);
 }
 
+// ---- LDS-tiled remap (packed map): one workgroup per 64 x 16 output tile ----------------------------
+// The direct kernel gathers ~24 scattered dwords per quad through the texture path, two dependent
+// round trips per wave (map, then source).  Here the source box a tile reads (precomputed once per
+// calibration by tile_box_kernel from the packed map) is staged in LDS by coalesced dword loads issued
+// together with the map loads -- one round trip -- and each pixel's two source rows are read from LDS;
+// a pixel with a tap outside its tile's box (image borders, or a box too large for LDS) takes
+// remap_blend's per-tap global path.  Same integer blend: bit-identical results.
+constexpr int kTileW = 64, kTileH = 16;      // 16 quads x 16 rows: one quad per thread of 256
+constexpr int kBoxMaxDw = 3072;              // 12 KB of LDS per workgroup for the box
+// Box word pair per tile: x = bx0 | by0 << 16, y = rowdw | h << 16 (rowdw = LDS dwords per staged row,
+// 0 = no box: every pixel of the tile takes the global path).  The staged row covers source bytes
+// [(bx0 cn) & ~3, (bx1 + 1) cn) plus two dwords of slack for the aligned three-dword reads.
+__global__ __launch_bounds__(256) void tile_box_kernel(const uint32_t* __restrict__ pmap, int W, int H, int sW, int sH,
+                                                       int cn, int tiles_x, uint2* __restrict__ boxes) {
+    __shared__ int red[4][4];
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int x0 = tx * kTileW + 4 * (threadIdx.x & 15), y = ty * kTileH + (threadIdx.x >> 4);
+    int lo_x = INT_MAX, hi_x = INT_MIN, lo_y = INT_MAX, hi_y = INT_MIN;
+    if (y < H)
+        for (int k = 0; k < 4 && x0 + k < W; ++k) {
+            const uint32_t w = pmap[(size_t)y * W + x0 + k];
+            const int sx = (int)((w >> 10) & 2047u) - 1, sy = (int)(w >> 21) - 1;
+            if (sx < sW && sx + 1 >= 0 && sy < sH && sy + 1 >= 0) {  // some tap in the source
+                lo_x = min(lo_x, sx);
+                hi_x = max(hi_x, sx + 1);
+                lo_y = min(lo_y, sy);
+                hi_y = max(hi_y, sy + 1);
+            }
+        }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo_x = min(lo_x, __shfl_xor(lo_x, o));
+        hi_x = max(hi_x, __shfl_xor(hi_x, o));
+        lo_y = min(lo_y, __shfl_xor(lo_y, o));
+        hi_y = max(hi_y, __shfl_xor(hi_y, o));
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[wv][0] = lo_x;
+        red[wv][1] = hi_x;
+        red[wv][2] = lo_y;
+        red[wv][3] = hi_y;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int k = 1; k < 4; ++k) {
+        lo_x = min(red[0][0], red[k][0]);
+        red[0][0] = lo_x;
+        red[0][1] = max(red[0][1], red[k][1]);
+        red[0][2] = min(red[0][2], red[k][2]);
+        red[0][3] = max(red[0][3], red[k][3]);
+    }
+    const int bx0 = max(red[0][0], 0), bx1 = min(red[0][1], sW - 1);
+    const int by0 = max(red[0][2], 0), by1 = min(red[0][3], sH - 1);
+    uint2 b = make_uint2(0u, 0u);
+    if (red[0][0] != INT_MAX && bx1 > bx0 && by1 > by0) {
+        const int rowdw = (((bx1 + 1) * cn + 3) >> 2) - ((bx0 * cn) >> 2) + 2;
+        const int h = by1 - by0 + 1;
+        if (rowdw <= 256 && rowdw * h <= kBoxMaxDw)
+            b = make_uint2((unsigned)bx0 | ((unsigned)by0 << 16), (unsigned)rowdw | ((unsigned)h << 16));
+    }
+    boxes[blockIdx.x] = b;
+}
+
+template <int CN>
+__global__ __launch_bounds__(256) void remap_tile_kernel(RemapJob j0, RemapJob j1, int sW, int sH, int W, int H,
+                                                         int tiles_x, unsigned tiles_per_job, const uint2* __restrict__ b0,
+                                                         const uint2* __restrict__ b1, int vec_dst) {
+    constexpr int NWD = CN == 1 ? 2 : 3;
+    __shared__ uint32_t box[kBoxMaxDw];
+    const unsigned lb = xcd_block(blockIdx.x, gridDim.x);
+    const unsigned job = lb >= tiles_per_job ? 1u : 0u;
+    const RemapJob& j = job ? j1 : j0;
+    const unsigned tile = lb - job * tiles_per_job;
+    const uint2 b = (job ? b1 : b0)[tile];
+    const int tx = (int)(tile % (unsigned)tiles_x), ty = (int)(tile / (unsigned)tiles_x);
+    const int x0 = tx * kTileW + 4 * (int)(threadIdx.x & 15), y = ty * kTileH + (int)(threadIdx.x >> 4);
+    const int bx0 = (int)(b.x & 0xFFFFu), by0 = (int)(b.x >> 16), rowdw = (int)(b.y & 0xFFFFu), bh = (int)(b.y >> 16);
+    // last column whose bytes are all staged (and in the image: the staged row may run past sW - 1)
+    const int bx1 = rowdw ? min((4 * (rowdw - 2) + ((bx0 * CN) & ~3)) / CN - 1, sW - 1) : -1;
+    const int by1 = by0 + bh - 1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(j.src), (short)0, (int)((unsigned)sH * (unsigned)j.spitch), 0x00020000);
+    // 1. the box (coalesced dwords; bytes past the last source byte read as 0) and the map, in flight together
+    if (rowdw) {
+        const int per = 256 / rowdw;
+        const int t = (int)threadIdx.x, r0 = t / rowdw, c = t - r0 * rowdw;
+        const uint32_t base = (uint32_t)((bx0 * CN) & ~3) + 4u * (uint32_t)c;
+        if (r0 < per)
+            for (int r = r0; r < bh; r += per)
+                box[r * rowdw + c] =
+                    __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(by0 + r) * (uint32_t)j.spitch + base, 0, 0);
+    }
+    const bool live = y < H && x0 < W;
+    const int n = live ? min(4, W - x0) : 0;
+    int mx[4], my[4], mf[4];
+    {
+        uint32_t w4[4] = {0u, 0u, 0u, 0u};
+        if (live) {
+            const size_t mrow = (size_t)y * W + x0;
+            if (n == 4 && (W & 3) == 0) {
+                const uint4 m = *reinterpret_cast<const uint4*>(j.pmap + mrow);
+                w4[0] = m.x; w4[1] = m.y; w4[2] = m.z; w4[3] = m.w;
+            } else {
+                for (int k = 0; k < 4; ++k) w4[k] = j.pmap[mrow + (k < n ? k : 0)];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mf[k] = (int)(w4[k] & 1023u);
+            mx[k] = (int)((w4[k] >> 10) & 2047u) - 1;
+            my[k] = (int)(w4[k] >> 21) - 1;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    // 2. each pixel whose four taps lie in the box reads its two rows' aligned dwords from LDS
+    uint32_t u0[4][NWD], u1[4][NWD];
+    uint32_t good = 0;
+    const int bbase = (bx0 * CN) & ~3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int sx = mx[k], sy = my[k];
+        const bool in = rowdw && sx >= bx0 && sx + 1 <= bx1 && sy >= by0 && sy + 1 <= by1;
+        good |= in ? 1u << k : 0u;
+        const int r = in ? sy - by0 : 0;
+        const int di = in ? r * rowdw + ((((sx * CN) & ~3) - bbase) >> 2) : 0;
+#pragma unroll
+        for (int i = 0; i < NWD; ++i) {
+            u0[k][i] = box[di + i];
+            u1[k][i] = box[di + rowdw + i];
+        }
+    }
+    uint32_t out[4 * CN];
+    remap_blend<CN>(j, sW, sH, mx, my, mf, u0, u1, good, out);
+    uint8_t* d = j.dst + (size_t)y * j.dpitch + (size_t)x0 * CN;
+    if (vec_dst && n == 4) {
+        if constexpr (CN == 3) {
+            uint3 w;
+            w.x = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+            w.y = out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24);
+            w.z = out[8] | (out[9] << 8) | (out[10] << 16) | (out[11] << 24);
+            *reinterpret_cast<uint3*>(d) = w;
+        } else {
+            *reinterpret_cast<uint32_t*>(d) = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+        }
+    } else {
+        for (int q = 0; q < n * CN; ++q) d[q] = (uint8_t)out[q];
+    }
+}
+
+usv_status launch_remap_tiled(const RemapJob& a, const RemapJob& b, const uint2* ba, const uint2* bb, int n_jobs,
+                              int cn, int sW, int sH, int W, int H, hipStream_t s) {
+    bool vec_dst = true;
+    for (int i = 0; i < n_jobs; ++i) {
+        const RemapJob& j = i ? b : a;
+        vec_dst = vec_dst && aligned(j.dst, 4) && (j.dpitch % 4) == 0;
+        if (!aligned(j.pmap, 16)) return USV_ERR_INVALID_ARG;
+    }
+    if ((long long)sH * a.spitch >= (1LL << 31) || (long long)sH * b.spitch >= (1LL << 31)) return USV_ERR_UNSUPPORTED;
+    const int tiles_x = (W + kTileW - 1) / kTileW, tiles_y = (H + kTileH - 1) / kTileH;
+    const unsigned per_job = (unsigned)tiles_x * (unsigned)tiles_y;
+    dim3 grid(per_job * (unsigned)n_jobs), block(256);
+    if (cn == 1)
+        hipLaunchKernelGGL(remap_tile_kernel<1>, grid, block, 0, s, a, b, sW, sH, W, H, tiles_x, per_job, ba, bb,
+                           (int)vec_dst);
+    else if (cn == 3)
+        hipLaunchKernelGGL(remap_tile_kernel<3>, grid, block, 0, s, a, b, sW, sH, W, H, tiles_x, per_job, ba, bb,
+                           (int)vec_dst);
+    else
+        return USV_ERR_UNSUPPORTED;
+    return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
+}
+
 bool job_ok(const RemapJob& j, int cn, int sW, int W) {
     return j.src && (j.pmap || (j.map1 && j.map2)) && j.dst && j.spitch >= sW * cn && j.dpitch >= W * cn;
 }
@@ -266,6 +439,43 @@ usv_status usv_rectify_pair_packed_u8(const uint8_t* srcL, const uint8_t* srcR, 
     const usv::RemapJob b{srcR, spitch, nullptr, nullptr, dstR, dpitch, pmapR};
     if (!usv::job_ok(a, cn, sW, W) || !usv::job_ok(b, cn, sW, W)) return USV_ERR_INVALID_ARG;
     return usv::launch_remap(a, b, 2, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+usv_status usv_remap_tile_boxes(const uint32_t* pmap, int W, int H, int sW, int sH, int cn, uint32_t* boxes,
+                                void* stream) {
+    if (!pmap || !boxes || W <= 0 || H <= 0 || sW <= 0 || sH <= 0) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    if (!usv::packed_ok(sW, sH) || H > 65535) return USV_ERR_UNSUPPORTED;
+    const int tiles_x = (W + usv::kTileW - 1) / usv::kTileW, tiles_y = (H + usv::kTileH - 1) / usv::kTileH;
+    hipLaunchKernelGGL(usv::tile_box_kernel, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), pmap, W, H, sW, sH, cn, tiles_x, reinterpret_cast<uint2*>(boxes));
+    return hipGetLastError() == hipSuccess ? USV_OK : USV_ERR_HIP;
+}
+
+usv_status usv_remap_packed_tiled_u8(const uint8_t* src, int sW, int sH, int spitch, int cn, const uint32_t* pmap,
+                                     const uint32_t* boxes, int W, int H, uint8_t* dst, int dpitch, void* stream) {
+    if (!pmap || !boxes || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535) return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    if (!usv::packed_ok(sW, sH)) return USV_ERR_UNSUPPORTED;
+    usv::RemapJob j{src, spitch, nullptr, nullptr, dst, dpitch, pmap};
+    if (!usv::job_ok(j, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    const uint2* b = reinterpret_cast<const uint2*>(boxes);
+    return usv::launch_remap_tiled(j, j, b, b, 1, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
+}
+
+usv_status usv_rectify_pair_packed_tiled_u8(const uint8_t* srcL, const uint8_t* srcR, int sW, int sH, int spitch,
+                                            int cn, const uint32_t* pmapL, const uint32_t* pmapR,
+                                            const uint32_t* boxesL, const uint32_t* boxesR, int W, int H,
+                                            uint8_t* dstL, uint8_t* dstR, int dpitch, void* stream) {
+    if (!pmapL || !pmapR || !boxesL || !boxesR || sW <= 0 || sH <= 0 || W <= 0 || H <= 0 || H > 65535)
+        return USV_ERR_INVALID_ARG;
+    if (cn != 1 && cn != 3) return USV_ERR_UNSUPPORTED;
+    if (!usv::packed_ok(sW, sH)) return USV_ERR_UNSUPPORTED;
+    const usv::RemapJob a{srcL, spitch, nullptr, nullptr, dstL, dpitch, pmapL};
+    const usv::RemapJob b{srcR, spitch, nullptr, nullptr, dstR, dpitch, pmapR};
+    if (!usv::job_ok(a, cn, sW, W) || !usv::job_ok(b, cn, sW, W)) return USV_ERR_INVALID_ARG;
+    return usv::launch_remap_tiled(a, b, reinterpret_cast<const uint2*>(boxesL), reinterpret_cast<const uint2*>(boxesR),
+                                   2, cn, sW, sH, W, H, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

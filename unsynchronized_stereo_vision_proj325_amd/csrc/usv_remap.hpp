@@ -68,6 +68,59 @@ __device__ __forceinline__ unsigned xcd_block(unsigned lin, unsigned total) {
     return xcd * base + min(xcd, rem) + (lin >> 3);
 }
 
+// The bilinear blend of a quad from its two source rows' aligned dwords (u0, u1: NWD dwords per pixel
+// starting at (sx * CN) & ~3) where bit k of `good` says pixel k's dwords are the exact ones and all
+// four taps lie in the source; the other pixels are redone from j.src tap by tap, 0 outside
+// (BORDER_CONSTANT).  Shared by the direct remap (remap_quad) and the LDS-tiled one (usv_rectify.hip).
+template <int CN>
+__device__ __forceinline__ void remap_blend(const RemapJob& j, int sW, int sH, const int (&mx)[4], const int (&my)[4],
+                                            const int (&mf)[4], const uint32_t (&u0)[4][CN == 1 ? 2 : 3],
+                                            const uint32_t (&u1)[4][CN == 1 ? 2 : 3], uint32_t good,
+                                            uint32_t (&out)[4 * CN]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t ty = (uint32_t)mf[k] >> 5, tx = (uint32_t)mf[k] & 31u;
+        // row weights as u16 pairs: (32 - tx, tx) scaled by (32 - ty) for row 0, by ty for row 1
+        const uint32_t wx = (32u - tx) | (tx << 16);
+        const uint32_t wr0 = wx * (32u - ty), wr1 = wx * ty;  // both halves <= 1024: no carry
+        const int o = (mx[k] * CN) & 3;
+        const uint32_t l0 = __builtin_amdgcn_alignbyte(u0[k][1], u0[k][0], o);  // tap bytes 0..3
+        const uint32_t l1 = __builtin_amdgcn_alignbyte(u1[k][1], u1[k][0], o);
+        uint32_t h0 = 0, h1 = 0;
+        if constexpr (CN == 3) {
+            h0 = __builtin_amdgcn_alignbyte(u0[k][2], u0[k][1], o);  // tap bytes 4..7
+            h1 = __builtin_amdgcn_alignbyte(u1[k][2], u1[k][1], o);
+        }
+#pragma unroll
+        for (int c = 0; c < CN; ++c) {
+            // (left tap | right tap << 16) of each row: byte c and byte CN + c of (h:l); v_perm bytes 0-3
+            // are its second operand, 4-7 its first, 0x0c gives zero
+            const uint32_t sel = 0x0c000c00u | (uint32_t)c | ((uint32_t)(CN + c) << 16);
+            const uint32_t p0 = __builtin_amdgcn_perm(h0, l0, sel);
+            const uint32_t p1 = __builtin_amdgcn_perm(h1, l1, sel);
+            out[k * CN + c] = remap_dot2(p0, wr0, remap_dot2(p1, wr1, 1u << 9)) >> 10;
+        }
+        if (!(good >> k & 1u)) {
+            // border / clamped read: per-tap reads, 0 outside (BORDER_CONSTANT), all four outside -> 0
+            const int sx = mx[k], sy = my[k];
+            const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
+            const bool any = sx < sW && sx + 1 >= 0 && sy < sH && sy + 1 >= 0;
+            const uint8_t* rp0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
+            const uint8_t* rp1 = rp0 + j.spitch;
+            const uint32_t w0 = wr0 & 0xFFFFu, w1 = wr0 >> 16, w2 = wr1 & 0xFFFFu, w3 = wr1 >> 16;
+#pragma unroll
+            for (int c = 0; c < CN; ++c) {
+                const uint32_t v0 = (any && x0ok && y0ok) ? rp0[c] : 0;
+                const uint32_t v1 = (any && x1ok && y0ok) ? rp0[CN + c] : 0;
+                const uint32_t v2 = (any && x0ok && y1ok) ? rp1[c] : 0;
+                const uint32_t v3 = (any && x1ok && y1ok) ? rp1[CN + c] : 0;
+                out[k * CN + c] =
+                    (__umul24(v0, w0) + __umul24(v1, w1) + __umul24(v2, w2) + __umul24(v3, w3) + (1u << 9)) >> 10;
+            }
+        }
+    }
+}
+
 // One quad: output pixels (y, x0 .. x0 + n - 1) of job j into out[4 * CN] (channel-interleaved).
 //   * Loads first: the map (one 16-B and one 8-B load when the rows are 4-pixel aligned), then for
 //     every pixel the two aligned source reads (2 dwords for gray, 3 for BGR per row) at an address
@@ -168,48 +221,7 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
         }
 #endif
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t ty = (uint32_t)mf[k] >> 5, tx = (uint32_t)mf[k] & 31u;
-        // row weights as u16 pairs: (32 - tx, tx) scaled by (32 - ty) for row 0, by ty for row 1
-        const uint32_t wx = (32u - tx) | (tx << 16);
-        const uint32_t wr0 = wx * (32u - ty), wr1 = wx * ty;  // both halves <= 1024: no carry
-        const int o = (mx[k] * CN) & 3;
-        const uint32_t l0 = __builtin_amdgcn_alignbyte(u0[k][1], u0[k][0], o);  // tap bytes 0..3
-        const uint32_t l1 = __builtin_amdgcn_alignbyte(u1[k][1], u1[k][0], o);
-        uint32_t h0 = 0, h1 = 0;
-        if constexpr (CN == 3) {
-            h0 = __builtin_amdgcn_alignbyte(u0[k][2], u0[k][1], o);  // tap bytes 4..7
-            h1 = __builtin_amdgcn_alignbyte(u1[k][2], u1[k][1], o);
-        }
-#pragma unroll
-        for (int c = 0; c < CN; ++c) {
-            // (left tap | right tap << 16) of each row: byte c and byte CN + c of (h:l); v_perm bytes 0-3
-            // are its second operand, 4-7 its first, 0x0c gives zero
-            const uint32_t sel = 0x0c000c00u | (uint32_t)c | ((uint32_t)(CN + c) << 16);
-            const uint32_t p0 = __builtin_amdgcn_perm(h0, l0, sel);
-            const uint32_t p1 = __builtin_amdgcn_perm(h1, l1, sel);
-            out[k * CN + c] = remap_dot2(p0, wr0, remap_dot2(p1, wr1, 1u << 9)) >> 10;
-        }
-        if (!(good >> k & 1u)) {
-            // border / clamped read: per-tap reads, 0 outside (BORDER_CONSTANT), all four outside -> 0
-            const int sx = mx[k], sy = my[k];
-            const bool x0ok = sx >= 0, x1ok = sx + 1 < sW, y0ok = sy >= 0, y1ok = sy + 1 < sH;
-            const bool any = sx < sW && sx + 1 >= 0 && sy < sH && sy + 1 >= 0;
-            const uint8_t* rp0 = j.src + (ptrdiff_t)sy * j.spitch + (ptrdiff_t)sx * CN;
-            const uint8_t* rp1 = rp0 + j.spitch;
-            const uint32_t w0 = wr0 & 0xFFFFu, w1 = wr0 >> 16, w2 = wr1 & 0xFFFFu, w3 = wr1 >> 16;
-#pragma unroll
-            for (int c = 0; c < CN; ++c) {
-                const uint32_t v0 = (any && x0ok && y0ok) ? rp0[c] : 0;
-                const uint32_t v1 = (any && x1ok && y0ok) ? rp0[CN + c] : 0;
-                const uint32_t v2 = (any && x0ok && y1ok) ? rp1[c] : 0;
-                const uint32_t v3 = (any && x1ok && y1ok) ? rp1[CN + c] : 0;
-                out[k * CN + c] =
-                    (__umul24(v0, w0) + __umul24(v1, w1) + __umul24(v2, w2) + __umul24(v3, w3) + (1u << 9)) >> 10;
-            }
-        }
-    }
+    remap_blend<CN>(j, sW, sH, mx, my, mf, u0, u1, good, out);
 }
 
 }  // namespace usv

@@ -51,10 +51,16 @@ class Rectifier:
 
     PACK_MAX_SRC = 2046  # include/usv.h usv_remap_pack_map
 
+    TILE_W, TILE_H = 64, 16  # include/usv.h usv_remap_tile_boxes
+
     def __init__(self, K, dist, R, P, size: tuple[int, int], device=None, stream=None,
-                 src_size: tuple[int, int] | None = None, packed: bool = True):
+                 src_size: tuple[int, int] | None = None, packed: bool = True, tiled: bool = True):
         """size: output (W, H); src_size: the frames' (W, H) (default: size, as initUndistortRectifyMap's
-        callers use it, P/Main.cpp:352); packed: also build the packed map when the source allows."""
+        callers use it, P/Main.cpp:352); packed: also build the packed map when the source allows; tiled:
+        remap packed frames through the LDS-tiled kernel (source boxes per 64 x 16 tile, built once per
+        channel count on first use; bit-identical to the direct packed remap)."""
+        self.tiled = tiled
+        self._boxes = {}
         self.W, self.H = int(size[0]), int(size[1])
         self.sW, self.sH = (self.W, self.H) if src_size is None else (int(src_size[0]), int(src_size[1]))
         self.params = rectify_params(K, dist, R, P)
@@ -74,6 +80,17 @@ class Rectifier:
                     self.map1.data_ptr(), self.map2.data_ptr(), self.W, self.H, self.sW, self.sH,
                     self.pmap.data_ptr(), _stream(stream)))
 
+    def boxes(self, cn: int, stream=None) -> torch.Tensor:
+        """The packed map's per-tile source boxes for cn-channel frames (usv_remap_tile_boxes), cached."""
+        if cn not in self._boxes:
+            tiles = ((self.W + self.TILE_W - 1) // self.TILE_W) * ((self.H + self.TILE_H - 1) // self.TILE_H)
+            b = torch.empty((tiles, 2), dtype=torch.int32, device=self.pmap.device)
+            with torch.cuda.device(self.pmap.device):
+                _lib.check("usv_remap_tile_boxes", _lib.load().usv_remap_tile_boxes(
+                    self.pmap.data_ptr(), self.W, self.H, self.sW, self.sH, cn, b.data_ptr(), _stream(stream)))
+            self._boxes[cn] = b
+        return self._boxes[cn]
+
     def packed_for(self, src: torch.Tensor) -> bool:
         """True when frames of src's size go through the packed map."""
         return self.pmap is not None and (src.shape[1], src.shape[0]) == (self.sW, self.sH)
@@ -90,6 +107,13 @@ class Rectifier:
                               device=src.device)
         _check_u8(out, "out")
         lib = _lib.load()
+        if self.packed_for(src) and self.tiled:
+            boxes = self.boxes(cn, stream)
+            with torch.cuda.device(src.device):
+                _lib.check("usv_remap_packed_tiled_u8", lib.usv_remap_packed_tiled_u8(
+                    src.data_ptr(), src.shape[1], src.shape[0], src.stride(0), cn, self.pmap.data_ptr(),
+                    boxes.data_ptr(), self.W, self.H, out.data_ptr(), out.stride(0), _stream(stream)))
+            return out
         if self.packed_for(src):
             with torch.cuda.device(src.device):
                 _lib.check("usv_remap_packed_u8", lib.usv_remap_packed_u8(
@@ -119,6 +143,14 @@ def rectify_pair(left: Rectifier, right: Rectifier, src_l: torch.Tensor, src_r: 
     if out_l.stride() != out_r.stride():
         raise ValueError("the two outputs must share strides")
     lib = _lib.load()
+    if left.packed_for(src_l) and right.packed_for(src_r) and left.tiled and right.tiled:
+        bl, br = left.boxes(cn, stream), right.boxes(cn, stream)
+        with torch.cuda.device(src_l.device):
+            _lib.check("usv_rectify_pair_packed_tiled_u8", lib.usv_rectify_pair_packed_tiled_u8(
+                src_l.data_ptr(), src_r.data_ptr(), src_l.shape[1], src_l.shape[0], src_l.stride(0), cn,
+                left.pmap.data_ptr(), right.pmap.data_ptr(), bl.data_ptr(), br.data_ptr(), left.W, left.H,
+                out_l.data_ptr(), out_r.data_ptr(), out_l.stride(0), _stream(stream)))
+        return out_l, out_r
     if left.packed_for(src_l) and right.packed_for(src_r):
         with torch.cuda.device(src_l.device):
             _lib.check("usv_rectify_pair_packed_u8", lib.usv_rectify_pair_packed_u8(
