@@ -24,6 +24,7 @@
 
 #include "usv_band.hpp"
 #include "usv_kernels.hpp"
+#include "usv_tiles.hpp"
 
 namespace usv {
 namespace {
@@ -327,30 +328,30 @@ __global__ __launch_bounds__(64, USV_GROUP_OCC) void sad_group_kernel(const uint
                                                                      const uint8_t* __restrict__ R,
                                                                      uint8_t* __restrict__ disp,
                                                                      double* __restrict__ dist, MatchArgs a,
-                                                                     GroupPlan P) {
+                                                                     GroupPlan P, const uint2* __restrict__ tiles) {
     using C = GCfg<RAD, G>;
     __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
-    // work map of sad_pair_kernel: XCD k owns the k-th contiguous run of tiles (x-tile fastest, then
-    // band, then pair); band heights weighted by dispatch generation
-    const unsigned total = gridDim.x, lin = blockIdx.x;
-    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-    const unsigned tile = xcd * base + min(xcd, rem) + (lin >> 3);
-    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
-    const bool past = tile >= per_pair && P.extra > 0;
-    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
-    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
-    const unsigned pair = past ? 0u : tile / per_pair;
-    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
-    const unsigned long_run = base + 1u, split = rem * long_run;
-    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
-                                  (unsigned)P.gen_g, P.weights);
-    const unsigned pre = bs.pre, tot = bs.tot;
-    const int xt = (int)col_xt;
+    // work map of sad_pair_kernel (usv_tiles.hpp): XCD k owns the k-th contiguous run of tiles (x-tile
+    // fastest, then band, then pair); normally one scalar load from the launcher's table
+    unsigned xtu, pair;
+    int y_begin, y_end;
+    if (tiles) {
+        const uint2 t = tiles[blockIdx.x];
+        xtu = t.x & 0xFFFFu;
+        pair = t.x >> 16;
+        y_begin = (int)(t.y & 0xFFFFu);
+        y_end = (int)(t.y >> 16);
+    } else {
+        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P.n_xt, P.m, P.extra, P.gen_g, P.weights, a.H);
+        xtu = sp.xt;
+        pair = sp.pair;
+        y_begin = sp.y_begin;
+        y_end = sp.y_end;
+    }
+    const int xt = (int)xtu;
     // the last tile is aligned to the right border (it may overlap its neighbour; both write the same values)
     const int x0 = xt == P.n_xt - 1 ? a.W - C::KW : xt * C::KW;
-    const int y_begin = (int)((unsigned long long)a.H * pre / tot);
-    const int y_end = (int)((unsigned long long)a.H * (pre + bs.own) / tot);
     L += (size_t)pair * a.pair_stride;
     R += (size_t)pair * a.pair_stride;
     disp += (size_t)pair * a.disp_stride;
@@ -410,8 +411,9 @@ hipError_t launch_group_rg(const MatchArgs& a, hipStream_t s) {
     P.gen_g = (int)(4L * (group_cu_count() / 8));
     if (P.gen_g < 1) P.gen_g = 1;
     P.weights = per_cu == 12 && total > 2L * 8 * P.gen_g ? USV_GROUP_WEIGHTS : 0x01010101u;
+    const uint2* tiles = tile_table(2, RAD * 16 + G, a, P.n_xt, P.m, P.extra, P.gen_g, P.weights, (unsigned)total, s);
     hipLaunchKernelGGL((sad_group_kernel<RAD, G>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist,
-                       a, P);
+                       a, P, tiles);
     return hipGetLastError();
 }
 

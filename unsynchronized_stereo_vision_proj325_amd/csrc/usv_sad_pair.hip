@@ -4,12 +4,8 @@
 // Spec: SURVEY.md §8(a) A1 (restated in oracle/sad_oracle.c); DESIGN.md §3 has the derivation.  The
 // reference has no block matcher; its nearest primitive is the u8 absdiff motion mask
 // at P/Main.cpp:304.  Integer arithmetic only: bit-exact with the oracle by construction.
-#include <array>
-#include <map>
-#include <mutex>
-#include <vector>
-
 #include "usv_sad_common.hpp"
+#include "usv_tiles.hpp"
 
 namespace usv {
 namespace {
@@ -483,30 +479,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #endif
 constexpr int pair_occ(int rad, int) { return rad >= 7 ? USV_PAIR_OCC7 : USV_PAIR_OCC5; }
 
-// Work map of one launch (the sad_fast_kernel map: XCD-contiguous tile runs, generation-weighted
-// bands): workgroup `lin` of `total` -> its x-tile, pair and output rows.  Host and device run the
-// same function: the launcher tabulates it once per launch geometry (tile_table), so a workgroup
-// normally reads its span with one scalar load instead of ~500 SALU of divisions and band sums.
-struct TileSpan {
-    unsigned xt, pair;
-    int y_begin, y_end;
-};
-__host__ __device__ __forceinline__ TileSpan tile_span(unsigned lin, unsigned total, const BandPlan& P, int H) {
-    const unsigned xcd = lin & 7u, base = total >> 3, rem = total & 7u;
-    const unsigned tile = xcd * base + (xcd < rem ? xcd : rem) + (lin >> 3);
-    const unsigned nxt = (unsigned)P.n_xt, per_pair = nxt * (unsigned)P.m;
-    const bool past = tile >= per_pair && P.extra > 0;
-    const unsigned col_xt = past ? tile - per_pair : tile % nxt;
-    const unsigned s = past ? (unsigned)P.m : (tile / nxt) % (unsigned)P.m;
-    const unsigned pair = past ? 0u : tile / per_pair;
-    const unsigned m_col = (unsigned)P.m + (col_xt < (unsigned)P.extra ? 1u : 0u);
-    const unsigned long_run = base + 1u, split = rem * long_run;
-    const BandSpan bs = band_span(pair, per_pair, nxt, col_xt, s, m_col, base, long_run, split,
-                                  (unsigned)P.gen_g, P.weights);
-    return TileSpan{col_xt, pair, (int)((unsigned long long)H * bs.pre / bs.tot),
-                    (int)((unsigned long long)H * (bs.pre + bs.own) / bs.tot)};
-}
-
 template <int RAD, int NW>
 __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(const uint8_t* __restrict__ L,
                                                               const uint8_t* __restrict__ R,
@@ -526,7 +498,7 @@ __global__ __launch_bounds__(NW * 64, pair_occ(RAD, NW)) void sad_pair_kernel(co
         y_begin = (int)(t.y & 0xFFFFu);
         y_end = (int)(t.y >> 16);
     } else {
-        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P, a.H);
+        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P.n_xt, P.m, P.extra, P.gen_g, P.weights, a.H);
         xtu = sp.xt;
         pair = sp.pair;
         y_begin = sp.y_begin;
@@ -583,38 +555,6 @@ int resident_pair_blocks_per_cu() {
 #define USV_PAIR_GEN_WEIGHTS_NW2 0x41415564u  // 100, 85, 65, 65
 #endif
 
-// The work map of a launch geometry as a device table (one uint2 per workgroup), built on the host
-// from tile_span and uploaded once (synchronously) per geometry and device; immutable afterwards, so
-// any stream may read it.  nullptr (the kernel computes its span itself) while the stream is being
-// captured into a graph and the geometry has no table yet, or when a field does not fit 16 bits.
-const uint2* tile_table(int rad, int nw, const MatchArgs& a, const BandPlan& P, unsigned total, hipStream_t s) {
-    if (a.H > 0xFFFF || P.n_xt > 0xFFFF || a.batch > 0xFFFF) return nullptr;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    const std::array<long long, 11> key{dev, rad, nw, a.W, a.H, a.batch, P.n_xt, P.m, P.extra,
-                                        ((long long)P.gen_g << 32) | P.weights, total};
-    static std::mutex mu;
-    static std::map<std::array<long long, 11>, uint2*> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    std::vector<uint2> host(total);
-    for (unsigned lin = 0; lin < total; ++lin) {
-        const TileSpan sp = tile_span(lin, total, P, a.H);
-        host[lin] = make_uint2(sp.xt | (sp.pair << 16), (unsigned)sp.y_begin | ((unsigned)sp.y_end << 16));
-    }
-    uint2* d = nullptr;
-    if (hipMalloc(&d, total * sizeof(uint2)) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, host.data(), total * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    cache.emplace(key, d);
-    return d;
-}
-
 template <int RAD, int NW>
 hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     constexpr int K = PCfg<RAD, NW>::K, WIN = 2 * RAD + 1;
@@ -643,7 +583,7 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
               : NW > 1 ? USV_PAIR_GEN_WEIGHTS_NW2
               : kPairPipe<RAD> ? USV_PAIR_GEN_WEIGHTS : USV_PAIR_GEN_WEIGHTS_UNPIPED;
     dim3 grid((unsigned)total), block(NW * 64);
-    const uint2* tiles = tile_table(RAD, NW, a, P, (unsigned)total, s);
+    const uint2* tiles = tile_table(1, RAD * 16 + NW, a, P.n_xt, P.m, P.extra, P.gen_g, P.weights, (unsigned)total, s);
     hipLaunchKernelGGL((sad_pair_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P, tiles);
     return hipGetLastError();
 }
