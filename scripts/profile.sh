@@ -27,5 +27,14 @@ run pmc_cyc --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_
 run pmc_cyc2 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_FLAT SQ_INSTS_LDS
 run pmc_grbm --pmc GRBM_GUI_ACTIVE GRBM_COUNT
 run pmc_icache --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQC_DCACHE_HITS SQC_DCACHE_MISSES
+# cold-cache passes (a 512 MiB write between launches, scripts/prof_cold.py): HBM bytes per launch
+if [ -n "$COLD" ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    n=pmc_cold_$(echo $c | tr 'A-Z' 'a-z')
+    echo "=== $n ($(date +%T))"
+    timeout -k 10 240 rocprofv3 --pmc $c -d $OUT/$n -o $n --output-format csv -- python3 scripts/prof_cold.py $COLD 10 \
+       > $OUT/$n.log 2>&1 || { echo "FAILED $n"; exit 1; }
+  done
+fi
 run pmc_fifo --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_INST_LEVEL_LDS SQ_LDS_ADDR_CONFLICT
 exit 0

@@ -71,27 +71,36 @@ def main():
         d = os.path.join(src, p)
         if p.startswith("pmc_") and os.path.isdir(d):
             got = counters(d, a.kernel)
+            if p.startswith("pmc_cold_"):  # cold-cache launches (scripts/prof_cold.py)
+                got = {k + "_cold": v for k, v in got.items()}
             c.update(got)
             if got:
                 shutil.copy(next(os.path.join(d, f) for f in os.listdir(d) if f.endswith("counter_collection.csv")),
                             os.path.join(dst, f"{p}.csv"))
 
-    fetch_b = c.get("FETCH_SIZE", 0.0) * 1024 * a.fetch_factor  # KiB -> B, calibrated
-    write_b = c.get("WRITE_SIZE", 0.0) * 1024
-    hbm = fetch_b + write_b if "FETCH_SIZE" in c and "WRITE_SIZE" in c else None
+    # HBM bytes: the cold-cache passes when present (inputs evicted before every launch), else the
+    # bench's back-to-back launches (inputs may stay in L2 / Infinity Cache between launches)
+    cold = "FETCH_SIZE_cold" in c and "WRITE_SIZE_cold" in c
+    fk, wk = ("FETCH_SIZE_cold", "WRITE_SIZE_cold") if cold else ("FETCH_SIZE", "WRITE_SIZE")
+    fetch_b = c.get(fk, 0.0) * 1024 * a.fetch_factor  # KiB -> B, calibrated
+    write_b = c.get(wk, 0.0) * 1024
+    hbm = fetch_b + write_b if fk in c and wk in c else None
     entry = {
         "kernel": dom["Name"],
         "avg_ns": avg_ns,
         "calls": int(dom["Calls"]),
-        "fetch_bytes_per_launch": fetch_b if "FETCH_SIZE" in c else None,
-        "fetch_size_kib_raw": c.get("FETCH_SIZE"),
+        "fetch_bytes_per_launch": fetch_b if fk in c else None,
+        "fetch_size_kib_raw": c.get(fk),
+        "cache_state": "cold (512 MiB write between launches)" if cold else "warm (back-to-back bench launches)",
         "fetch_factor": a.fetch_factor,
-        "write_bytes_per_launch": write_b if "WRITE_SIZE" in c else None,
+        "write_bytes_per_launch": write_b if wk in c else None,
         "bytes_per_launch": hbm,
         "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
         "counters": c,
         "source": f"profiles/{a.tag}/ (rocprofv3 --kernel-trace --stats; separate --pmc passes; "
-                  f"bytes = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE, KiB x 1024)",
+                  f"bytes = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE, KiB x 1024, "
+                  f"{'cold-cache launches' if cold else 'bench launches'}; FETCH factor from "
+                  f"profiles/probes_r04/traffic_calibration_r04.md)",
     }
     table = os.path.join(ROOT, "profiles", "counters.json")
     allc = json.load(open(table)) if os.path.exists(table) else {}
@@ -108,7 +117,7 @@ def main():
     for k in sorted(c):
         lines.append(f"| {k} | {c[k]:.6g} |")
     if hbm is not None:
-        lines += ["", f"HBM bytes per launch = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE = {hbm/1e6:.2f} MB "
+        lines += ["", f"HBM bytes per launch ({'cold' if cold else 'warm'}) = {a.fetch_factor:g} x {fk} + {wk} = {hbm/1e6:.2f} MB "
                       f"({hbm / (avg_ns * 1e-9) / 1e9:.0f} GB/s over the {avg_ns/1e3:.1f} µs average)"]
     if c.get("SQ_INSTS_VALU"):
         lane_ops = c["SQ_INSTS_VALU"] * 64
