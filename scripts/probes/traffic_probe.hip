@@ -85,12 +85,15 @@ __global__ __launch_bounds__(kBlock) void rd_buf_ubyte(const uint8_t* __restrict
     if (lds[threadIdx.x] == 0x12345678u) out[0] = 1;
 }
 
+// each wave reads its own contiguous 4 KiB chunks (no 128-B line shared by two XCDs' L2s)
 __global__ __launch_bounds__(64) void rd_sload_x8(const uint8_t* __restrict__ p, size_t n, uint32_t* out) {
     typedef uint32_t su8 __attribute__((ext_vector_type(8)));
     uint32_t acc = 0;
-    for (size_t c = (size_t)blockIdx.x * 32; c < n; c += (size_t)gridDim.x * 32) {
+    for (size_t c = (size_t)blockIdx.x * 4096; c < n; c += (size_t)gridDim.x * 4096)
+    for (size_t k = 0; k < 4096; k += 32) {
+        const size_t cc = c + k;
         su8 v;
-        asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p + c) : "memory");
+        asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p + cc) : "memory");
         acc ^= v[0] ^ v[7];
     }
     if (acc == 0x12345678u && threadIdx.x == 0) out[0] = acc;
@@ -142,7 +145,7 @@ int main() {
         hipLaunchKernelGGL(rd_buf_ubyte, grid, blk, 0, 0, buf, kBytes, out);
         CHECK(hipDeviceSynchronize());
         CHECK(flush());
-        hipLaunchKernelGGL(rd_sload_x8, dim3(cus * 32), dim3(64), 0, 0, buf, kBytes, out);
+        hipLaunchKernelGGL(rd_sload_x8, dim3(cus * 16), dim3(64), 0, 0, buf, kBytes, out);
         CHECK(hipDeviceSynchronize());
         CHECK(flush());
         hipLaunchKernelGGL(wr_store_x4, grid, blk, 0, 0, reinterpret_cast<uint4*>(buf), kBytes / 16);

@@ -35,6 +35,10 @@ if [ -n "$COLD" ]; then
     timeout -k 10 240 rocprofv3 --pmc $c -d $OUT/$n -o $n --output-format csv -- python3 scripts/prof_cold.py $COLD 10 \
        > $OUT/$n.log 2>&1 || { echo "FAILED $n"; exit 1; }
   done
+  # read requests by size (L2 -> fabric): true read bytes = 32*n32 + 64*n64 + 128*n128
+  n=pmc_cold_rdreq; echo "=== $n ($(date +%T))"
+  timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+     -d $OUT/$n -o $n --output-format csv -- python3 scripts/prof_cold.py $COLD 10 > $OUT/$n.log 2>&1 || echo "optional pass $n failed"
 fi
 run pmc_fifo --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_INST_LEVEL_LDS SQ_LDS_ADDR_CONFLICT
 exit 0

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""FETCH_SIZE / WRITE_SIZE calibration from scripts/gpu_traffic_probe.sh's passes
+(gpurun_out/traffic/{fetch,write,rdreq}): per probe kernel, the median per-dispatch counter over its
+launches against the 64 MiB it moved, written to profiles/probes_r04/traffic_calibration_r04.md."""
+import csv
+import glob
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "traffic")
+BYTES = 64 << 20
+FORMS = {
+    "rd_vload_x4": "global_load_dwordx4 to VGPRs, 16 B per lane (the guide's reference form)",
+    "rd_glds_x4": "global_load_lds_dwordx4, 16 B per lane (distance-table staging)",
+    "rd_glds_ubyte": "global_load_lds_ubyte, 1 B per lane, 64 consecutive bytes per instruction",
+    "rd_buf_ubyte": "buffer_load_ubyte ... lds (the paired kernel's steady-state R-row DMA)",
+    "rd_sload_x8": "s_load_dwordx8, 32 B per wave instruction (L-row segment form)",
+    "wr_store_x4": "global_store_dwordx4, 16 B per lane",
+    "wr_store_b64": "global_store_dwordx2, 8 B per lane (disparity flush store)",
+}
+
+
+def per_kernel(pass_name):
+    out = defaultdict(lambda: defaultdict(list))
+    for fn in glob.glob(os.path.join(SRC, pass_name, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(fn)):
+            name = row["Kernel_Name"]
+            for k in FORMS:
+                if k in name:
+                    out[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: statistics.median(v) for c, v in d.items()} for k, d in out.items()}
+
+
+fetch, write, rdreq = per_kernel("fetch"), per_kernel("write"), per_kernel("rdreq")
+lines = ["# FETCH_SIZE / WRITE_SIZE calibration (round 4)", "",
+         "`scripts/probes/traffic_probe.hip` under `scripts/gpu_traffic_probe.sh`: every probe kernel moves exactly "
+         f"{BYTES >> 20} MiB once, after a 512 MiB write that evicts the L2s and the Infinity Cache; counters are the "
+         "median per-dispatch value over 3 launches (rocprofv3 --pmc, one counter per pass).  factor = bytes moved / "
+         "(counter KiB x 1024): multiply a kernel's counter by the factor of its access form to get HBM bytes.", "",
+         "| kernel | form | FETCH_SIZE KiB | fetch factor | WRITE_SIZE KiB | write factor | TCC_EA0_RDREQ | RDREQ_32B |",
+         "|---|---|---|---|---|---|---|---|"]
+for k, form in FORMS.items():
+    f = fetch.get(k, {}).get("FETCH_SIZE")
+    w = write.get(k, {}).get("WRITE_SIZE")
+    rq = rdreq.get(k, {})
+    ff = f"{BYTES / (f * 1024):.3f}" if f else "—"
+    wf = f"{BYTES / (w * 1024):.3f}" if (w and k.startswith('wr')) else "—"
+    lines.append(f"| `{k}` | {form} | {f if f is not None else '—'} | {ff} | {w if w is not None else '—'} | {wf} | "
+                 f"{rq.get('TCC_EA0_RDREQ_sum', '—')} | {rq.get('TCC_EA0_RDREQ_32B_sum', '—')} |")
+txt = "\n".join(lines) + "\n"
+dst = os.path.join(ROOT, "profiles", "probes_r04", "traffic_calibration_r04.md")
+os.makedirs(os.path.dirname(dst), exist_ok=True)
+open(dst, "w").write(txt)
+print(txt)

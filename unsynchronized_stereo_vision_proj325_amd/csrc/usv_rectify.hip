@@ -234,15 +234,26 @@ __global__ __launch_bounds__(256) void remap_tile_kernel(RemapJob j0, RemapJob j
     const int by1 = by0 + bh - 1;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(j.src), (short)0, (int)((unsigned)sH * (unsigned)j.spitch), 0x00020000);
-    // 1. the box (coalesced dwords; bytes past the last source byte read as 0) and the map, in flight together
+    // 1. the box (coalesced dwords) and the map, in flight together.  A dword wholly past the last source
+    // byte reads as 0 (never used); the one dword that straddles the end is read byte by byte, since a
+    // buffer load returns 0 for a dword that is only partly in range.
     if (rowdw) {
         const int per = 256 / rowdw;
         const int t = (int)threadIdx.x, r0 = t / rowdw, c = t - r0 * rowdw;
         const uint32_t base = (uint32_t)((bx0 * CN) & ~3) + 4u * (uint32_t)c;
+        const uint32_t lim = (uint32_t)sH * (uint32_t)j.spitch;
         if (r0 < per)
-            for (int r = r0; r < bh; r += per)
-                box[r * rowdw + c] =
-                    __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(by0 + r) * (uint32_t)j.spitch + base, 0, 0);
+            for (int r = r0; r < bh; r += per) {
+                const uint32_t off = (uint32_t)(by0 + r) * (uint32_t)j.spitch + base;
+                uint32_t v;
+                if (off + 4u <= lim || off >= lim) {
+                    v = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+                } else {
+                    v = 0;
+                    for (uint32_t q = 0; q < 4u && off + q < lim; ++q) v |= (uint32_t)j.src[off + q] << (8u * q);
+                }
+                box[r * rowdw + c] = v;
+            }
     }
     const bool live = y < H && x0 < W;
     const int n = live ? min(4, W - x0) : 0;
