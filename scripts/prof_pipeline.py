@@ -15,8 +15,8 @@ W, H = 1920, 1080
 rng = np.random.default_rng(0)
 cl, cr = synthetic_calibration(W, H, seed=1)
 rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
-# the direct (untiled) packed remap beside the tiled default: both kernels in the same trace
-dl, dr = Rectifier(*cl, (W, H), device=dev, tiled=False), Rectifier(*cr, (W, H), device=dev, tiled=False)
+# the opt-in LDS-tiled packed remap beside the direct default: both kernels in the same trace
+dl, dr = Rectifier(*cl, (W, H), device=dev, tiled=True), Rectifier(*cr, (W, H), device=dev, tiled=True)
 src = [torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev) for _ in range(2)]
 prep = FramePrep(dev)
 gray = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(dev)

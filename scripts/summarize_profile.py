@@ -83,6 +83,11 @@ def main():
     cold = "FETCH_SIZE_cold" in c and "WRITE_SIZE_cold" in c
     fk, wk = ("FETCH_SIZE_cold", "WRITE_SIZE_cold") if cold else ("FETCH_SIZE", "WRITE_SIZE")
     fetch_b = c.get(fk, 0.0) * 1024 * a.fetch_factor  # KiB -> B, calibrated
+    # read requests by size (cold pass): exact for every load form (profiles/probes_r04/traffic_calibration_r04.md)
+    sized = cold and all(f"TCC_EA0_RDREQ_{z}B_sum_cold" in c for z in (32, 64, 128))
+    if sized:
+        fetch_b = sum(z * c[f"TCC_EA0_RDREQ_{z}B_sum_cold"] for z in (32, 64, 128))
+    how = ("32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B" if sized else f"{a.fetch_factor:g} x {fk}")
     write_b = c.get(wk, 0.0) * 1024
     hbm = fetch_b + write_b if fk in c and wk in c else None
     entry = {
@@ -92,14 +97,15 @@ def main():
         "fetch_bytes_per_launch": fetch_b if fk in c else None,
         "fetch_size_kib_raw": c.get(fk),
         "cache_state": "cold (512 MiB write between launches)" if cold else "warm (back-to-back bench launches)",
-        "fetch_factor": a.fetch_factor,
+        "fetch_factor": None if sized else a.fetch_factor,
+        "fetch_method": how,
         "write_bytes_per_launch": write_b if wk in c else None,
         "bytes_per_launch": hbm,
         "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
         "counters": c,
         "source": f"profiles/{a.tag}/ (rocprofv3 --kernel-trace --stats; separate --pmc passes; "
-                  f"bytes = {a.fetch_factor:g} x FETCH_SIZE + WRITE_SIZE, KiB x 1024, "
-                  f"{'cold-cache launches' if cold else 'bench launches'}; FETCH factor from "
+                  f"read bytes = {how}, write bytes = WRITE_SIZE KiB x 1024, "
+                  f"{'cold-cache launches' if cold else 'bench launches'}; calibration in "
                   f"profiles/probes_r04/traffic_calibration_r04.md)",
     }
     table = os.path.join(ROOT, "profiles", "counters.json")
@@ -117,7 +123,7 @@ def main():
     for k in sorted(c):
         lines.append(f"| {k} | {c[k]:.6g} |")
     if hbm is not None:
-        lines += ["", f"HBM bytes per launch ({'cold' if cold else 'warm'}) = {a.fetch_factor:g} x {fk} + {wk} = {hbm/1e6:.2f} MB "
+        lines += ["", f"HBM bytes per launch ({'cold' if cold else 'warm'}) = {how} + {wk} = {hbm/1e6:.2f} MB "
                       f"({hbm / (avg_ns * 1e-9) / 1e9:.0f} GB/s over the {avg_ns/1e3:.1f} µs average)"]
     if c.get("SQ_INSTS_VALU"):
         lane_ops = c["SQ_INSTS_VALU"] * 64
