@@ -163,6 +163,82 @@ def test_no_sgpr_use_while_scalar_load_in_flight(fast_kernels):
     assert not any(bad.values()), {k: v for k, v in bad.items() if v}
 
 
+def _vregs(tok):
+    tok = tok.rstrip(",")
+    m = re.match(r"v\[(\d+):(\d+)\]$", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+_LGKM = ("ds_", "s_load", "s_buffer_load", "s_sendmsg")
+
+
+def inflight_lds_read_hazards(ins, cap=64):
+    """Instructions that touch a VGPR while an LDS read writing it may still be in flight.
+
+    The paired kernel's staged-entry reads can be hand-written ds_read_b64 (USV_PAIR_RDASM) that the
+    compiler's waitcnt pass does not see, retired by explicit counted lgkmcnt waits; a register the
+    compiler believes free (e.g. the never-read half of the last pair) would be clobbered by the late
+    return.  Forward dataflow over the CFG with the ordered list of outstanding LGKM operations (LDS
+    reads carry their destination VGPRs, other LGKM operations none): lgkmcnt(n) keeps the n newest.
+    """
+    succ = _successors(ins)
+    state = [None] * len(ins)
+    state[0] = ()
+    work, bad = [0], set()
+
+    def join(a, b):
+        n = max(len(a), len(b))
+        a, b = ((frozenset(),) * (n - len(a)) + a, (frozenset(),) * (n - len(b)) + b)
+        return tuple(x | y for x, y in zip(a, b))
+
+    while work:
+        k = work.pop()
+        cur, i = list(state[k]), ins[k]
+        toks = i.replace(",", " ").split()
+        pend = set().union(*cur) if cur else set()
+        if i.startswith("s_waitcnt") and "lgkmcnt" in i:
+            n = int(re.search(r"lgkmcnt\((\d+)\)", i).group(1))
+            cur = cur[len(cur) - n:] if n > 0 else []
+        elif i.startswith(_LGKM):
+            touched = set().union(*(_vregs(t) for t in toks[1:])) if len(toks) > 1 else set()
+            if touched & pend:
+                bad.add((k, str(i)))
+            dst = _vregs(toks[1]) if i.startswith("ds_read") and len(toks) > 1 else set()
+            cur.append(frozenset(dst))
+            cur = cur[-cap:]
+        elif i.startswith("v_"):
+            if set().union(*(_vregs(t) for t in toks[1:])) & pend:
+                bad.add((k, str(i)))
+        fs = tuple(cur)
+        for j in succ[k]:
+            new = fs if state[j] is None else join(state[j], fs)
+            if state[j] is None or new != state[j]:
+                state[j] = new
+                work.append(j)
+    return sorted(bad)
+
+
+def test_no_vgpr_use_while_lds_read_in_flight(fast_kernels):
+    pair = {k: v for k, v in fast_kernels.items() if "sad_pair_kernel" in k}
+    bad = {k: inflight_lds_read_hazards(v)[:3] for k, v in pair.items()}
+    assert not any(bad.values()), {k: v for k, v in bad.items() if v}
+
+
+def test_lds_read_hazard_checker_catches_a_clobber():
+    # the round-4 defect this check exists for: the never-read half of a pending pair reused
+    ins = [Insn(t, 4 * n) for n, t in enumerate([
+        "ds_read_b64 v[10:11], v44", "ds_read_b64 v[28:29], v44 offset:72", "s_waitcnt lgkmcnt(1)",
+        "v_sad_u8 v29, s40, v11, 0", "s_waitcnt lgkmcnt(0)", "s_endpgm"])]
+    assert [k for k, _ in inflight_lds_read_hazards(ins)] == [3]
+    ok = [Insn(t, 4 * n) for n, t in enumerate([
+        "ds_read_b64 v[10:11], v44", "ds_write_b32 v1, v2", "s_waitcnt lgkmcnt(1)", "v_add_u32_e32 v3, v10, v11",
+        "s_endpgm"])]
+    assert inflight_lds_read_hazards(ok) == []
+
+
 def test_lds_dma_m0_wait_state(fast_kernels):
     # GFX9: an SALU write of M0 needs one wait state before an LDS-DMA reads it
     for name, ins in fast_kernels.items():

@@ -47,6 +47,12 @@ struct PCfg {
     // so in the WIN-unrolled row loop every slot, LDS offset and M0 value is a compile-time constant;
     // 12 waves x 13.0 KB fit the CU's 160 KB).  Otherwise 8 slots indexed t & 7 (r = 6, 7 or two waves
     // per workgroup would not fit WIN slots at three waves per SIMD).
+#ifndef USV_PAIR_RDASM
+#define USV_PAIR_RDASM 1  // staged-entry reads as single ds_read_b64 (inline asm, explicit lgkmcnt waits): C 51.70 -> 49.32 us
+#endif
+#ifndef USV_PAIR_ADDTID
+#define USV_PAIR_ADDTID 1  // transpose stores as ds_write_addtid_b32 (C 52.33 -> 51.77 us, E 511.9 -> 508.0 us)
+#endif
 #ifndef USV_PAIR_STATIC
 #define USV_PAIR_STATIC 1
 #endif
@@ -82,6 +88,14 @@ struct PCfg {
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
 };
+
+typedef uint32_t u2x __attribute__((ext_vector_type(2)));
+typedef uint32_t u4x __attribute__((ext_vector_type(4)));
+// one ds_read_b64 the compiler cannot pair or count (USV_PAIR_RDASM): the caller waits for it explicitly
+template <uint32_t OFF>
+__device__ __forceinline__ void ds_read_b64_at(u2x& v, uint32_t addr) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+}
 
 template <int RAD, int NW, int EDGE>
 __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
@@ -161,6 +175,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     LWords lw_next;
     auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
 
+    u4x trq[2];  // the pipelined argmin's transposed words (tr_issue -> tr_piece)
+    const uint32_t ra0 = lds_addr(rbuf + s_l);  // this lane's first staged entry in slot 0
     auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int I = decltype(i_tag)::value;
@@ -215,11 +231,35 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         uint32_t E[C::NE_V];
         constexpr int NV = C::NE_V / C::VEC, NV1 = C::SPLIT > 1 ? (NV + 1) / 2 : NV;
         constexpr int J1 = C::SPLIT > 1 ? NV1 * C::VEC - 1 : NPOS;  // steps the first batch completes
+        // USV_PAIR_RDASM: the entries as NV single ds_read_b64 (2 LDS cycles each; the compiler pairs plain
+        // 8-byte reads into ds_read2_b64 at 8 cycles per pair, MI355X_MICROARCH.md LDS table).  They are
+        // invisible to the compiler's wait counting, so the first chain step that needs pair k is preceded
+        // by an explicit counted lgkmcnt wait between two scheduling barriers (in-order LDS returns;
+        // nothing else is outstanding in lgkm but the compiler's own later LDS ops, which only make a wait
+        // stricter).  The previous row's transposed words are retired first (an asm that redefines them),
+        // so the compiler has no pending read left to drain with a lgkmcnt(0) of its own.
+        // (1: single-batch rows, r <= 6; 2: also r = 7's two batches, which spill 24 B at two waves)
+        constexpr bool RDASM = C::VEC == 2 && (USV_PAIR_RDASM == 2 || (USV_PAIR_RDASM == 1 && C::SPLIT == 1));
+        u2x ev[NV];
+        constexpr uint32_t BOFF = C::STATIC ? 4u * (uint32_t)(I * C::NRS) : 0u;
+        uint32_t ra = ra0;
+        if constexpr (RDASM && !C::STATIC) ra += 4u * (uint32_t)boff;
+        auto issue_reads = [&](auto k0t, auto k1t) {
+            constexpr int k0 = decltype(k0t)::value, k1 = decltype(k1t)::value;
+            [&]<int... Kk>(std::integer_sequence<int, Kk...>) {
+                (ds_read_b64_at<BOFF + 8u * (k0 + Kk)>(ev[k0 + Kk], ra), ...);
+            }(std::make_integer_sequence<int, k1 - k0>{});
+        };
+        if constexpr (RDASM) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]) : : "memory");
+            issue_reads(std::integral_constant<int, 0>{}, std::integral_constant<int, NV1>{});
+        } else {
 #pragma unroll
-        for (int k = 0; k < NV1; ++k) {
-            const VT v = rb[k];
+            for (int k = 0; k < NV1; ++k) {
+                const VT v = rb[k];
 #pragma unroll
-            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+                for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+            }
         }
         // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half).  With the argmin
         // pipelined, piece j of the previous row's argmin follows chain step j and the pair is
@@ -228,6 +268,20 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         A[0] = 0;
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
+            if constexpr (RDASM && (j == 0 || (j & 1))) {  // first step that needs pair k
+                constexpr int k = (j + 1) / 2;
+                constexpr int later = k < NV1 ? NV1 - 1 - k : NV - 1 - k;  // reads of its batch issued after it
+                // lgkmcnt(later), vmcnt / expcnt left at their maxima; the scheduling barriers keep the
+                // pair's uses below the wait (the compiler believes the asm outputs ready at once)
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F | (later << 8));
+                // both registers of the pair stay allocated until here even when one is never read (the last
+                // pair's second entry): a register the compiler thought free would be overwritten by the load
+                asm volatile("" ::"v"(ev[k]));
+                __builtin_amdgcn_sched_barrier(0);
+                E[2 * k] = ev[k].x;
+                E[2 * k + 1] = ev[k].y;
+            }
             const uint32_t l = lbyte(j);
             A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
             pre(jt);
@@ -236,7 +290,14 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         [&]<int... J>(std::integer_sequence<int, J...>) {
             (chain_step(std::integral_constant<int, J>{}), ...);
         }(std::make_integer_sequence<int, J1>{});
-        if constexpr (C::SPLIT > 1) {
+        if constexpr (C::SPLIT > 1 && RDASM) {
+            static_assert(!kPairPipe<RAD>, "the second batch's chain steps carry no argmin pieces");
+            __builtin_amdgcn_sched_barrier(0);
+            issue_reads(std::integral_constant<int, NV1>{}, std::integral_constant<int, NV>{});
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (chain_step(std::integral_constant<int, J1 + J>{}), ...);
+            }(std::make_integer_sequence<int, NPOS - J1>{});
+        } else if constexpr (C::SPLIT > 1) {
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int k = NV1; k < NV; ++k) {
@@ -334,16 +395,29 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     //              lanes 8q .. 8q + 7 (two ds_read_b128) -- nothing waits on them here;
     //   tr_finish: 16 keys (cost << 8) | d by v_perm, a v_min3 tree, three DPP rounds across the 8
     //              lanes of the pixel, one comb word per pixel.
-    uint4 trq[2];
+    const uint32_t tb_lds = lds_addr(tb);
     auto tr_issue = [&](const uint32_t(&S)[K]) {
+        if constexpr (USV_PAIR_ADDTID) {
+            // ds_write_addtid_b32: address = M0 + offset + 4 lane, no address VGPR; 2 LDS cycles per store
+            // against 6 for each ds_write2st64_b32 pair (MI355X_MICROARCH.md LDS table)
+            static_assert(K == 8, "eight transpose stores");
+            asm volatile("s_mov_b32 m0, %8\n\ts_nop 0\n\t"
+                         "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:256\n\t"
+                         "ds_write_addtid_b32 %2 offset:512\n\tds_write_addtid_b32 %3 offset:768\n\t"
+                         "ds_write_addtid_b32 %4 offset:1024\n\tds_write_addtid_b32 %5 offset:1280\n\t"
+                         "ds_write_addtid_b32 %6 offset:1536\n\tds_write_addtid_b32 %7 offset:1792"
+                         :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
+                            "s"(tb_lds) : "memory", "m0");
+        } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+            for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             // (r = 7: the second window's index is rebuilt per row as well)
             const uint32_t ri = (C::SPLIT > 1 && j == 1) ? (rdw[0] ^ 1u) : rdw[j];
-            trq[j] = reinterpret_cast<const uint4*>(tb)[ri];
+            trq[j] = reinterpret_cast<const u4x*>(tb)[ri];
         }
         asm volatile("" ::: "memory");
     };
