@@ -251,7 +251,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             }(std::make_integer_sequence<int, k1 - k0>{});
         };
         if constexpr (RDASM) {
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]) : : "memory");
+            // (pipelined argmin only: otherwise the words are consumed within their own row, and keeping
+            // them live into the next row costs r = 7 its last free registers)
+            if constexpr (kPairPipe<RAD>) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]) : : "memory");
             issue_reads(std::integral_constant<int, 0>{}, std::integral_constant<int, NV1>{});
         } else {
 #pragma unroll
