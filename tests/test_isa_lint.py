@@ -222,7 +222,7 @@ def inflight_lds_read_hazards(ins, cap=64):
 
 
 def test_no_vgpr_use_while_lds_read_in_flight(fast_kernels):
-    asm_reads = {k: v for k, v in fast_kernels.items() if "sad_pair_kernel" in k or "sad_group_kernel" in k}
+    asm_reads = {k: v for k, v in fast_kernels.items() if "sad_pair_kernel" in k or "sad_group_kernel" in k or "ssd_fast_kernel" in k}
     bad = {k: inflight_lds_read_hazards(v)[:3] for k, v in asm_reads.items()}
     assert not any(bad.values()), {k: v for k, v in bad.items() if v}
 

@@ -23,6 +23,19 @@ namespace {
 //     steps.  Ties -> smallest d, as in the SAD kernels.
 // Integer arithmetic only: bit-exact with oracle/sad_oracle.c's SSD by construction.
 // ===================================================================================
+// LDS-cycle forms of the paired kernel (usv_sad_pair.hip), USV_SSD_LDSR: the staged
+// entries as single ds_read_b64 issued by inline asm with a counted wait before the first chain step that needs
+// each pair (the compiler pairs plain reads into ds_read2_b64), the transpose stores as ds_write_addtid_b32.
+#ifndef USV_SSD_LDSR
+#define USV_SSD_LDSR 1  // rocprof: config C SSD 108.0 -> 102.3 us
+#endif
+typedef uint32_t ssd_u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t ssd_u4 __attribute__((ext_vector_type(4)));
+template <uint32_t OFF>
+__device__ __forceinline__ void ssd_ds_read_b64(ssd_u2& v, uint32_t addr) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+}
+
 template <int RAD, int NW>
 struct SCfg {
     static constexpr int K = 8;
@@ -118,6 +131,8 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
     LWords lw_next;
     auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
     using VT = typename VecT<C::VEC>::T;
+    ssd_u4 trq[2];  // the pipelined argmin's transposed words
+    const uint32_t ra0 = lds_addr(rbuf + s_l);
 
     auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
         constexpr bool WARM = decltype(warm_tag)::value;
@@ -155,17 +170,38 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
         asm volatile("" : "+s"(boff));
         const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
         uint32_t E[C::NPOS_V];
+        constexpr bool LDSR = USV_SSD_LDSR && C::VEC == 2;
+        constexpr int NV = C::NPOS_V / 2;
+        ssd_u2 ev[NV];
+        if constexpr (LDSR) {
+            // the previous row's transposed words retired first (see usv_sad_pair.hip)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]) : : "memory");
+            const uint32_t ra = ra0 + 4u * (uint32_t)boff;
+            [&]<int... Kk>(std::integer_sequence<int, Kk...>) {
+                (ssd_ds_read_b64<8u * Kk>(ev[Kk], ra), ...);
+            }(std::make_integer_sequence<int, NV>{});
+        } else {
 #pragma unroll
-        for (int k = 0; k < C::NPOS_V / C::VEC; ++k) {
-            const VT v = rb[k];
+            for (int k = 0; k < C::NPOS_V / C::VEC; ++k) {
+                const VT v = rb[k];
 #pragma unroll
-            for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+                for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
+            }
         }
         // P[j + 1] = P[j] + (L_j - R_j)^2; H[x] is formed as soon as P[x + w] exists
         uint32_t A[NPOS + 1];
         A[0] = 0;
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
+            if constexpr (LDSR && (j & 1) == 0) {  // step j = 2k first needs pair k
+                constexpr int k = j / 2;
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F | ((NV - 1 - k) << 8));
+                asm volatile("" ::"v"(ev[k]));
+                __builtin_amdgcn_sched_barrier(0);
+                E[2 * k] = ev[k].x;
+                E[2 * k + 1] = ev[k].y;
+            }
             const int diff = (int)Lv[j] - (int)E[j];
             A[j + 1] = (uint32_t)((int)A[j] + __mul24(diff, diff));
             if constexpr (j + 1 >= WIN) {
@@ -244,13 +280,24 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
         y_chunk += rows;
         cb ^= 1;
     };
-    uint4 trq[2];
+    const uint32_t tb_lds = lds_addr(tb);
     auto tr_issue = [&](const uint32_t(&S)[K]) {
+        if constexpr (USV_SSD_LDSR && C::VEC == 2) {  // (NW = 1, 4: more VGPRs, a spill at r = 5, NW = 4)
+            static_assert(K == 8, "eight transpose stores");
+            asm volatile("s_mov_b32 m0, %8\n\ts_nop 0\n\t"
+                         "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:256\n\t"
+                         "ds_write_addtid_b32 %2 offset:512\n\tds_write_addtid_b32 %3 offset:768\n\t"
+                         "ds_write_addtid_b32 %4 offset:1024\n\tds_write_addtid_b32 %5 offset:1280\n\t"
+                         "ds_write_addtid_b32 %6 offset:1536\n\tds_write_addtid_b32 %7 offset:1792"
+                         :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
+                            "s"(tb_lds) : "memory", "m0");
+        } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+            for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
+        }
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 2; ++j) trq[j] = reinterpret_cast<const uint4*>(tb)[rdw[j]];
+        for (int j = 0; j < 2; ++j) trq[j] = reinterpret_cast<const ssd_u4*>(tb)[rdw[j]];
         asm volatile("" ::: "memory");
     };
     uint32_t fv[8], fb, fm;
