@@ -11,9 +11,6 @@
 #ifndef USV_REMAP_NT
 #define USV_REMAP_NT 0
 #endif
-#ifndef USV_REMAP_WIDE
-#define USV_REMAP_WIDE 0  // 1: a tap row's NWD dwords as one dwordx2 / dwordx3 buffer load
-#endif
 #ifndef USV_REMAP_BUF
 #define USV_REMAP_BUF 1  // source reads as raw-buffer loads: 32-bit offsets, no 64-bit address arithmetic
 #endif
@@ -209,28 +206,11 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
         // of a 64-bit address built per read
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t*>(j.src), (short)0, (int)0xFFFFFFFF, 0x00020000);
-#if USV_REMAP_WIDE
-        // one multi-dword load per tap row (buffer loads need only dword alignment): 2 instead of 2 * NWD
-        if constexpr (NWD == 3) {
-            typedef uint32_t v3u __attribute__((ext_vector_type(3)));
-            const v3u a0 = __builtin_bit_cast(v3u, __builtin_amdgcn_raw_buffer_load_b96(rs, r0, 0, 0));
-            const v3u a1 = __builtin_bit_cast(v3u, __builtin_amdgcn_raw_buffer_load_b96(rs, r1, 0, 0));
-            u0[k][0] = a0[0]; u0[k][1] = a0[1]; u0[k][2] = a0[2];
-            u1[k][0] = a1[0]; u1[k][1] = a1[1]; u1[k][2] = a1[2];
-        } else {
-            typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-            const v2u a0 = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(rs, r0, 0, 0));
-            const v2u a1 = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(rs, r1, 0, 0));
-            u0[k][0] = a0[0]; u0[k][1] = a0[1];
-            u1[k][0] = a1[0]; u1[k][1] = a1[1];
-        }
-#else
 #pragma unroll
         for (int i = 0; i < NWD; ++i) {
             u0[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r0 + 4u * (uint32_t)i, 0, 0);
             u1[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r1 + 4u * (uint32_t)i, 0, 0);
         }
-#endif
 #else
         const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
         const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r1);
