@@ -50,6 +50,9 @@ struct PCfg {
 #ifndef USV_PAIR_RDASM
 #define USV_PAIR_RDASM 1  // staged-entry reads as single ds_read_b64 (inline asm, explicit lgkmcnt waits): C 51.70 -> 49.32 us
 #endif
+#ifndef USV_PAIR_RDASM_GRP
+#define USV_PAIR_RDASM_GRP 1  // staged-entry pairs retired per counted wait
+#endif
 #ifndef USV_PAIR_ADDTID
 #define USV_PAIR_ADDTID 1  // transpose stores as ds_write_addtid_b32 (C 52.33 -> 51.77 us, E 511.9 -> 508.0 us)
 #endif
@@ -270,19 +273,27 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         A[0] = 0;
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
-            if constexpr (RDASM && (j == 0 || (j & 1))) {  // first step that needs pair k
-                constexpr int k = (j + 1) / 2;
-                constexpr int later = k < NV1 ? NV1 - 1 - k : NV - 1 - k;  // reads of its batch issued after it
+            // first step that needs pair k0; pairs are retired USV_PAIR_RDASM_GRP at a time (a group never spans
+            // the two read batches of r = 7)
+            constexpr int k0 = (j + 1) / 2, GRP = USV_PAIR_RDASM_GRP;
+            constexpr int bstart = k0 < NV1 ? 0 : NV1, bend = k0 < NV1 ? NV1 : NV;
+            if constexpr (RDASM && (j == 0 || (j & 1)) && (k0 - bstart) % GRP == 0) {
+                constexpr int k1 = k0 + GRP < bend ? k0 + GRP : bend;  // pairs [k0, k1)
+                constexpr int later = bend - k1;                        // reads of its batch issued after them
                 // lgkmcnt(later), vmcnt / expcnt left at their maxima; the scheduling barriers keep the
-                // pair's uses below the wait (the compiler believes the asm outputs ready at once)
+                // pairs' uses below the wait (the compiler believes the asm outputs ready at once)
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F | (later << 8));
-                // both registers of the pair stay allocated until here even when one is never read (the last
+                // both registers of a pair stay allocated until here even when one is never read (the last
                 // pair's second entry): a register the compiler thought free would be overwritten by the load
-                asm volatile("" ::"v"(ev[k]));
+#pragma unroll
+                for (int k = k0; k < k1; ++k) asm volatile("" ::"v"(ev[k]));
                 __builtin_amdgcn_sched_barrier(0);
-                E[2 * k] = ev[k].x;
-                E[2 * k + 1] = ev[k].y;
+#pragma unroll
+                for (int k = k0; k < k1; ++k) {
+                    E[2 * k] = ev[k].x;
+                    E[2 * k + 1] = ev[k].y;
+                }
             }
             const uint32_t l = lbyte(j);
             A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
