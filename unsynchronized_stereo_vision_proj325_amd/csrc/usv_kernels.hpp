@@ -24,7 +24,9 @@
     defined(USV_GROUP_OCC) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
     defined(USV_GROUP_WEIGHTS) || defined(USV_PREP_THREADS) || defined(USV_HSV_PK) || defined(USV_PREP_KU) ||    \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
-    defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD)
+    defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD) ||   \
+    defined(USV_PAIR_RDASM) || defined(USV_PAIR_RDASM_GRP) || defined(USV_PAIR_ADDTID) || defined(USV_GROUP_LDSR) || \
+    defined(USV_SSD_LDSR)
 #error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
 #endif
 #define USV_BUILD_KIND "product build"
