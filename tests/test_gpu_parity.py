@@ -458,6 +458,25 @@ def test_ssd_fast_max_cost_saturated(gpu):
     assert np.array_equal(got, oracle_sad(L, R, D, 15, "ssd", "naive"))
 
 
+@pytest.mark.parametrize("W,H,D,w", [(256, 48, 128, 11), (256, 40, 256, 15), (192, 40, 100, 13), (128, 32, 64, 9),
+                                     (128, 32, 32, 5), (160, 24, 91, 11)])
+def test_sad_max_cost_and_ties(gpu, W, H, D, w):
+    """255 against 0 everywhere: the largest SAD (w^2 x 255, 57 375 at w = 15) in every packed half, plus the
+    whole-word L operand's d-independent extra on interior r = 5 tiles, must neither carry into the other half nor
+    wrap; then all-equal costs (every disparity ties: the smallest d, 0, wins).  Paired, grouped and column-paired
+    kernels (odd D = 91 takes the column-paired kernel; D = 100 at w = 13)."""
+    L = np.full((H, W), 255, dtype=np.uint8)
+    R = np.zeros((H, W), dtype=np.uint8)
+    R[:, ::5] = 255  # some cheaper disparities so the argmin is not all ties
+    got = gpu_disp(gpu, L, R, D, w, kernel="fast")
+    ref = oracle_sad(L, R, D, w, "sad", "naive")
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    R[:] = 0
+    got = gpu_disp(gpu, L, R, D, w, kernel="fast")
+    assert np.array_equal(got, oracle_sad(L, R, D, w, "sad", "naive"))
+    assert not got.any()
+
+
 def test_cpu_tensors_rejected():
     L = torch.zeros((16, 16), dtype=torch.uint8)
     with pytest.raises(ValueError):
