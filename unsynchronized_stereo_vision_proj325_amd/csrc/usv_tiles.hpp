@@ -46,8 +46,11 @@ __host__ __device__ __forceinline__ TileSpan tile_span(unsigned lin, unsigned to
 inline const uint2* tile_table(int kind, int variant, const MatchArgs& a, int n_xt, int m, int extra, int gen_g,
                                unsigned weights, unsigned total, hipStream_t s) {
     if (a.H > 0xFFFF || n_xt > 0xFFFF || a.batch > 0xFFFF) return nullptr;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    // the launch's device is the stream's (the caller's current device may be another one)
+    int dev = 0, cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    dev = cur;
+    if (s != nullptr && hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
     const std::array<long long, 11> key{dev, kind, variant, a.W, a.H, a.batch, n_xt, m, extra,
                                         ((long long)gen_g << 32) | weights, total};
     static std::mutex mu;
@@ -63,11 +66,15 @@ inline const uint2* tile_table(int kind, int variant, const MatchArgs& a, int n_
         host[lin] = make_uint2(sp.xt | (sp.pair << 16), (unsigned)sp.y_begin | ((unsigned)sp.y_end << 16));
     }
     uint2* d = nullptr;
-    if (hipMalloc(&d, total * sizeof(uint2)) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, host.data(), total * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
+    if (dev != cur && hipSetDevice(dev) != hipSuccess) return nullptr;
+    bool ok = hipMalloc(&d, total * sizeof(uint2)) == hipSuccess;
+    // upload on the launch's own stream (a synchronous hipMemcpy would go through the legacy stream, which
+    // another thread's global-mode stream capture forbids), then wait for it: the table is immutable after
+    ok = ok && hipMemcpyAsync(d, host.data(), total * sizeof(uint2), hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+    if (!ok && d) (void)hipFree(d);
+    if (dev != cur) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
     cache.emplace(key, d);
     return d;
 }
