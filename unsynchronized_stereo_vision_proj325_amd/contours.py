@@ -56,11 +56,15 @@ def contour_pair_scores(desc_a: torch.Tensor, desc_b: torch.Tensor, stream=None)
 class ContourMatcherGPU:
     """usv_contour_matcher (include/usv.h): GenerateMatchingList on the device from host contour sets,
     selection and in-order compaction included, for up to max_contours contours and max_points points
-    per set (pinned staging and device buffers allocated once, on the current HIP device)."""
+    per set (pinned staging and device buffers allocated once, on the current HIP device).  The C matcher
+    serves one call at a time (include/usv.h); a lock serialises callers that share this object (the
+    module-level GenerateMatchingListGPU cache)."""
 
     def __init__(self, max_contours: int = 512, max_points: int = 1 << 16):
         import ctypes
+        import threading
         self._ct = ctypes
+        self._lock = threading.Lock()
         self.lib = _lib.load()
         self.max_contours, self.max_points = max_contours, max_points
         h = ctypes.c_void_p()
@@ -84,7 +88,12 @@ class ContourMatcherGPU:
         return max(n_a, n_b) <= self.max_contours and max(p_a, p_b) <= self.max_points
 
     def match_flat(self, pa, oa, pb, ob):
-        """Flattened int32 sets (as usv_generate_matching_list) -> ctypes usv_match array, count."""
+        """Flattened int32 sets (as usv_generate_matching_list) -> ctypes usv_match array, count.  The array
+        is this object's output buffer: valid until its next call."""
+        with self._lock:
+            return self._match_flat(pa, oa, pb, ob)
+
+    def _match_flat(self, pa, oa, pb, ob):
         ct = self._ct
         n_a, n_b = len(oa) - 1, len(ob) - 1
         cap = max(1, n_a * n_b)
@@ -100,11 +109,13 @@ class ContourMatcherGPU:
     def __call__(self, contours_l, contours_r):
         pa, oa = _flatten(contours_l)
         pb, ob = _flatten(contours_r)
-        out, n = self.match_flat(pa, oa, pb, ob)
-        return [(out[k].left_index, out[k].right_index, out[k].match_value) for k in range(n)]
+        with self._lock:  # the list is built before the output buffer can be reused
+            out, n = self._match_flat(pa, oa, pb, ob)
+            return [(out[k].left_index, out[k].right_index, out[k].match_value) for k in range(n)]
 
 
 _MATCHERS: dict[int, ContourMatcherGPU] = {}
+_MATCHERS_LOCK = __import__("threading").Lock()
 
 
 def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
@@ -119,9 +130,10 @@ def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     n = max(len(contours_l), len(contours_r))
     p = max(sum(len(c) for c in contours_l), sum(len(c) for c in contours_r))
-    m = _MATCHERS.get(idx)
-    if m is None or not m.fits(n, n, p, p):
-        with torch.cuda.device(idx):
-            m = ContourMatcherGPU(max(512, n), max(1 << 16, p))
-        _MATCHERS[idx] = m
+    with _MATCHERS_LOCK:
+        m = _MATCHERS.get(idx)
+        if m is None or not m.fits(n, n, p, p):
+            with torch.cuda.device(idx):
+                m = ContourMatcherGPU(max(512, n), max(1 << 16, p))
+            _MATCHERS[idx] = m
     return m(contours_l, contours_r)
