@@ -239,6 +239,18 @@ def test_lds_read_hazard_checker_catches_a_clobber():
     assert inflight_lds_read_hazards(ok) == []
 
 
+def test_every_m0_write_feeds_an_lds_dma_or_addtid_store(fast_kernels):
+    # The paired kernel's transpose stores (ds_write_addtid_b32) may address the LDS from the M0 value the row's
+    # DMA left (USV_PAIR_M0REUSE): no instruction may write M0 unless it feeds, within two instructions, an
+    # LDS-DMA or an addtid store (a compiler-inserted M0 write in between would redirect the stores).
+    for name, ins in fast_kernels.items():
+        for k, i in enumerate(ins):
+            if re.match(r"s_\w+ m0,", i):
+                nxt = ins[k + 1:k + 3]
+                assert any(n.startswith(("global_load_lds", "ds_write_addtid")) or
+                           (n.startswith("buffer_load") and n.endswith(" lds")) for n in nxt), (name, i, nxt)
+
+
 def test_lds_dma_m0_wait_state(fast_kernels):
     # GFX9: an SALU write of M0 needs one wait state before an LDS-DMA reads it
     for name, ins in fast_kernels.items():

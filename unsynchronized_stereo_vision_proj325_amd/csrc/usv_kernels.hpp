@@ -26,7 +26,7 @@
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
     defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD) ||   \
     defined(USV_PAIR_RDASM) || defined(USV_PAIR_RDASM_GRP) || defined(USV_PAIR_ADDTID) || defined(USV_GROUP_LDSR) || \
-    defined(USV_SSD_LDSR)
+    defined(USV_SSD_LDSR) || defined(USV_PAIR_M0REUSE)
 #error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
 #endif
 #define USV_BUILD_KIND "product build"

@@ -488,6 +488,18 @@ __device__ __forceinline__ void dma_row_buf_at(su4 rsrc, uint32_t soff, const ui
                      :: "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "s"(base), "s"(rsrc), "s"(soff),
                         "n"(OFF) : "memory", "m0", "scc");
 }
+// dma_row_buf_at (three DMAs) with the row offset clamp min(raw, last) computed between the M0 write and the
+// first DMA: the clamp is the one wait state the M0 write needs, so no s_nop (USV_PAIR_M0REUSE).
+template <uint32_t OFF>
+__device__ __forceinline__ void dma_row3_at_min(su4 rsrc, int raw, int last, const uint32_t (&vo)[3], uint32_t base) {
+    int soff;
+    asm volatile("s_add_u32 m0, %4, %8\n\ts_min_i32 %0, %6, %7\n\tbuffer_load_ubyte %1, %5, %0 offen lds\n\t"
+                 "buffer_load_ubyte %2, %5, %0 offen offset:256 lds\n\t"
+                 "buffer_load_ubyte %3, %5, %0 offen offset:512 lds"
+                 : "=&s"(soff)
+                 : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(base), "s"(rsrc), "s"(raw), "s"(last), "n"(OFF)
+                 : "memory", "m0", "scc");
+}
 template <int N>
 __device__ __forceinline__ typename SWords<N>::T s_load_words_off(const uint8_t* p, uint32_t off) {
     typename SWords<N>::T w;
