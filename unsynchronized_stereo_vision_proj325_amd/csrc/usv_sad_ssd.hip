@@ -442,7 +442,7 @@ int resident_ssd_blocks_per_cu() {
 }
 
 #ifndef USV_SSD_GEN_WEIGHTS
-#define USV_SSD_GEN_WEIGHTS 0x41415564u  // 100, 85, 65, 65 (the two-wave paired kernel's heights; not refitted)
+#define USV_SSD_GEN_WEIGHTS 0x46465A64u  // 100, 90, 70, 70: rocprof A/B at config C SSD 102.4 -> 97.7 us (100:75:50 118.0, 100:95:85 98.4)
 #endif
 template <int RAD, int NW>
 hipError_t launch_ssd_rn(const MatchArgs& a, hipStream_t s) {
