@@ -181,8 +181,13 @@ def inflight_lds_read_hazards(ins, cap=64):
     The paired kernel's staged-entry reads can be hand-written ds_read_b64 (USV_PAIR_RDASM) that the
     compiler's waitcnt pass does not see, retired by explicit counted lgkmcnt waits; a register the
     compiler believes free (e.g. the never-read half of the last pair) would be clobbered by the late
-    return.  Forward dataflow over the CFG with the ordered list of outstanding LGKM operations (LDS
-    reads carry their destination VGPRs, other LGKM operations none): lgkmcnt(n) keeps the n newest.
+    return.  Forward dataflow over the CFG with the ordered list of outstanding LDS operations (reads
+    carry their destination VGPRs, other LDS operations none).  LDS operations return in order, so
+    lgkmcnt(n) retires all but the n newest of them.  Scalar-memory loads and messages also count in
+    lgkmcnt but return out of order (GFX9): one of them may have returned while n LDS operations are
+    still pending, so they are NOT entries of the list -- counting one among "the n newest" would
+    wrongly retire the LDS read just older than it.  A pending scalar load can only make a counted wait
+    stricter for the LDS operations, never weaker, so leaving it out is the sound bound.
     """
     succ = _successors(ins)
     state = [None] * len(ins)
@@ -206,9 +211,10 @@ def inflight_lds_read_hazards(ins, cap=64):
             touched = set().union(*(_vregs(t) for t in toks[1:])) if len(toks) > 1 else set()
             if touched & pend:
                 bad.add((k, str(i)))
-            dst = _vregs(toks[1]) if i.startswith("ds_read") and len(toks) > 1 else set()
-            cur.append(frozenset(dst))
-            cur = cur[-cap:]
+            if i.startswith("ds_"):  # scalar loads / messages: out of order, not list entries (above)
+                dst = _vregs(toks[1]) if i.startswith("ds_read") and len(toks) > 1 else set()
+                cur.append(frozenset(dst))
+                cur = cur[-cap:]
         elif i.startswith("v_"):
             if set().union(*(_vregs(t) for t in toks[1:])) & pend:
                 bad.add((k, str(i)))
@@ -239,6 +245,21 @@ def test_lds_read_hazard_checker_catches_a_clobber():
     assert inflight_lds_read_hazards(ok) == []
 
 
+def test_lds_read_hazard_checker_scalar_loads_return_out_of_order():
+    # lgkmcnt(1) with a scalar load as the newest LGKM operation: the s_load may have returned first,
+    # leaving the second ds_read pending -- using its destination is a hazard (an in-order model that
+    # counted the s_load as "the one still pending" would have passed this)
+    bad = [Insn(t, 4 * n) for n, t in enumerate([
+        "ds_read_b64 v[10:11], v44", "ds_read_b64 v[28:29], v44 offset:72", "s_load_dwordx2 s[4:5], s[0:1], 0x0",
+        "s_waitcnt lgkmcnt(1)", "v_sad_u8 v30, s40, v28, 0", "s_waitcnt lgkmcnt(0)", "s_endpgm"])]
+    assert [k for k, _ in inflight_lds_read_hazards(bad)] == [4]
+    # an s_load between two reads: lgkmcnt(1) still retires the older read (LDS returns are in order)
+    ok = [Insn(t, 4 * n) for n, t in enumerate([
+        "ds_read_b64 v[10:11], v44", "s_load_dwordx2 s[4:5], s[0:1], 0x0", "ds_read_b64 v[28:29], v44 offset:72",
+        "s_waitcnt lgkmcnt(1)", "v_sad_u8 v30, s40, v11, 0", "s_waitcnt lgkmcnt(0)", "s_endpgm"])]
+    assert inflight_lds_read_hazards(ok) == []
+
+
 def test_every_m0_write_feeds_an_lds_dma_or_addtid_store(fast_kernels):
     # The paired kernel's transpose stores (ds_write_addtid_b32) may address the LDS from the M0 value the row's
     # DMA left (USV_PAIR_M0REUSE): no instruction may write M0 unless it feeds, within two instructions, an
@@ -249,6 +270,44 @@ def test_every_m0_write_feeds_an_lds_dma_or_addtid_store(fast_kernels):
                 nxt = ins[k + 1:k + 3]
                 assert any(n.startswith(("global_load_lds", "ds_write_addtid")) or
                            (n.startswith("buffer_load") and n.endswith(" lds")) for n in nxt), (name, i, nxt)
+
+
+def reaching_m0_writes(ins):
+    """Forward dataflow over the CFG: for each instruction, the set of M0 writes (indices) that reach it."""
+    succ = _successors(ins)
+    state = [None] * len(ins)
+    state[0] = frozenset()
+    work = [0]
+    while work:
+        k = work.pop()
+        out = frozenset({k}) if re.match(r"s_\w+ m0,", ins[k]) else state[k]
+        for j in succ[k]:
+            if state[j] is None or not out <= state[j]:
+                state[j] = out if state[j] is None else state[j] | out
+                work.append(j)
+    return state
+
+
+def test_addtid_stores_see_one_dma_m0(fast_kernels):
+    # ADVICE r04: the static ring's transpose stores (USV_PAIR_M0REUSE) take M0 from the row's LDS-DMA.  Every
+    # ds_write_addtid_b32 must be reached by exactly ONE M0 write on every CFG path, and that write must either
+    # be an s_mov of the store group itself (the non-reuse form) or the M0 of an LDS-DMA (the row DMA whose base
+    # the store's constant offset is computed against) -- never a join of different M0 values at a loop latch.
+    n_reuse = 0
+    for name, ins in fast_kernels.items():
+        reach = reaching_m0_writes(ins)
+        for k, i in enumerate(ins):
+            if not i.startswith("ds_write_addtid"):
+                continue
+            r = reach[k]
+            assert r is not None and len(r) == 1, (name, i, k, sorted(r or ()))
+            (w,) = r
+            nxt = ins[w + 1:w + 3]
+            feeds_dma = any(n.startswith("global_load_lds") or (n.startswith("buffer_load") and n.endswith(" lds"))
+                            for n in nxt)
+            assert feeds_dma or ins[w].startswith("s_mov_b32 m0"), (name, i, ins[w])
+            n_reuse += feeds_dma
+    assert n_reuse > 0  # the reuse form is present in the build under test
 
 
 def test_lds_dma_m0_wait_state(fast_kernels):
