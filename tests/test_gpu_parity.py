@@ -508,3 +508,40 @@ def test_band_sharded_frame_equals_full(gpu, world):
     parts = [match_band(m, Lt, Rt, k, world) for k in range(world)]
     assert torch.equal(torch.cat(parts, 0), full)
     assert sum(p.shape[0] for p in parts) == 1080 and band_range(1080, 0, world, 11)[2] == 0
+
+
+def test_bound_launcher_matches_compute_and_oracle(gpu):
+    # StereoBlockMatcher.bind (the pre-marshalled launcher bench.py steps with): the same C-ABI entry point,
+    # so every launch equals compute() and the oracle, for single pairs (with / without the distance map)
+    # and batches; bind() validates exactly as compute() does
+    L, R, _ = synthetic_pair(640, 200, 128, pair_index=3, noise=2)
+    Lt, Rt = torch.from_numpy(L).to(gpu), torch.from_numpy(R).to(gpu)
+    m = StereoBlockMatcher(128, 11)
+    ref = oracle_sad(L, R, 128, 11, "sad", "sliding", threads=THREADS)
+    lut = distance_lut_cm()
+    d1 = torch.zeros_like(Lt)
+    x1 = torch.zeros(Lt.shape, dtype=torch.float64, device=gpu)
+    go = m.bind(Lt, Rt, out_disp=d1, out_dist=x1)
+    d1.zero_()
+    x1.zero_()
+    for _ in range(3):
+        assert go() is d1
+    torch.cuda.synchronize()
+    got = d1.cpu().numpy()
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    dd = x1.cpu().numpy()
+    assert ((dd == lut[got]) | (np.isinf(dd) & np.isinf(lut[got]))).all()
+    d2 = torch.zeros_like(Lt)
+    m.bind(Lt, Rt, out_disp=d2)()
+    torch.cuda.synchronize()
+    assert torch.equal(d2, d1)
+    Lb, Rb = torch.stack([Lt, Rt]), torch.stack([Rt, Lt])
+    db = torch.zeros_like(Lb)
+    m.bind(Lb, Rb, out_disp=db)()
+    torch.cuda.synchronize()
+    assert torch.equal(db[0], d1)
+    assert torch.equal(db[1], m.compute(Rt, Lt))
+    with pytest.raises(ValueError):
+        m.bind(Lt, Rt[:, :320], out_disp=d1)
+    with pytest.raises(ValueError):
+        m.bind(Lt, Rt, out_disp=torch.zeros((200, 640), dtype=torch.int16, device=gpu))

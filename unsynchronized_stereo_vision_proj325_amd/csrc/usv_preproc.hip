@@ -99,7 +99,7 @@ static_assert(kPT % 256 == 0 && kPT <= 1024, "whole 256-bin groups of threads");
 // blk of nblk (a job's share of the grid) sweeps quads blk * kPT * kU + threadIdx.x + u * kPT; the
 // first sweep's loads are issued BEFORE prologue() (the block's table / LUT set-up, which ends in a
 // barrier every thread reaches), so the two latencies overlap instead of adding.
-template <typename LoadF, typename PrologueF, typename BodyF>
+template <int kU = kU, typename LoadF, typename PrologueF, typename BodyF>
 __device__ __forceinline__ void for_each_quad(int W, int H, bool vec4, int blk, int nblk, LoadF load,
                                               PrologueF prologue, BodyF body) {
     const int nq = (W + 3) >> 2;
@@ -196,6 +196,16 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
     }
 }
 
+// Quads per thread of the V-histogram pass: it only reads, so four quads' loads in flight per thread and half
+// the blocks (half the per-block LDS clears, barriers and bin flushes) -- a stand-alone probe of this pass at
+// 1080p ran 4.38 us at two quads per thread, 3.68 at four, 3.94 at eight, with a no-histogram floor of
+// 3.37 us at four (scripts/probes/hist_probe.hip, profiles/probes_r05/hist_probe_r05.txt): the LDS atomics are
+// not what binds it; interleaving copies over the banks (32 or 64 per block) was slower.
+#ifndef USV_HIST_KU
+#define USV_HIST_KU 4
+#endif
+constexpr int kUHist = USV_HIST_KU;
+
 // Histogram of V = max(B, G, R) only (RGB2HSV_b's v; P/Main.cpp:368 equalizes that channel): the
 // first pass of usv_frame_prep_u8 / _pair_u8, which reads the frame and writes nothing but the
 // workspace histograms (per-wave LDS copies, one global add per occupied bin and block, the other
@@ -210,7 +220,7 @@ __global__ __launch_bounds__(kPT) void v_hist_kernel(HistJob j0, HistJob j1, int
     __shared__ uint32_t lh[NWV][256];
     const int t = threadIdx.x, wv = t >> 6;
     const bool vec4 = vec && (W & 3) == 0;
-    for_each_quad(
+    for_each_quad<kUHist>(
         W, H, vec4, blk, blocks_per_job,
         [&](int y, int x, int n, bool v) { return load_px4(j.bgr, j.pitch, y, x, v, n); },
         [&] {
@@ -528,9 +538,9 @@ __global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
 }
 
 
-// one sweep of kU quads per thread, at most 4096 blocks (larger frames loop)
-int prep_blocks(int W, int H) {
-    const long long q = (long long)((W + 3) / 4) * H, per = (long long)kPT * kU;
+// one sweep of ku quads per thread, at most 4096 blocks (larger frames loop)
+int prep_blocks(int W, int H, int ku = kU) {
+    const long long q = (long long)((W + 3) / 4) * H, per = (long long)kPT * ku;
     return (int)std::min<long long>(4096, std::max<long long>(1, (q + per - 1) / per));
 }
 
@@ -584,9 +594,9 @@ usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_
     const int ve = vh && al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
                    gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) && usv::fits32(bgr_pitch, H);
     const usv::HistJob hj{bgr, pitch, nullptr, 0, static_cast<uint32_t*>(work)};
-    const int nb = usv::prep_blocks(W, H);
+    const int nb = usv::prep_blocks(W, H), nbh = usv::prep_blocks(W, H, usv::kUHist);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(nb), dim3(usv::kPT), 0, s, hj, hj, W, H, parity, nb, vh);
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(nbh), dim3(usv::kPT), 0, s, hj, hj, W, H, parity, nbh, vh);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     const usv::EqJob ej{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
                         bgr, pitch};
@@ -609,10 +619,10 @@ usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int 
     const int ve = vh && al4(hsvL) && al4(hsvR) && al4(bgr_outL) && al4(bgr_outR) && al4(grayL) && al4(grayR) &&
                    hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 && gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) &&
                    usv::fits32(bgr_pitch, H);
-    const int nb = usv::prep_blocks(W, H);
+    const int nb = usv::prep_blocks(W, H), nbh = usv::prep_blocks(W, H, usv::kUHist);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nb), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, nullptr, 0, wL},
-                       usv::HistJob{bgrR, pitch, nullptr, 0, wR}, W, H, parity, nb, vh);
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nbh), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, nullptr, 0, wL},
+                       usv::HistJob{bgrR, pitch, nullptr, 0, wR}, W, H, parity, nbh, vh);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     hipLaunchKernelGGL(usv::equalize_kernel<true>, dim3(2 * nb), dim3(usv::kPT), 0, s,
                        usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch, bgrL, pitch},

@@ -71,6 +71,16 @@ struct PCfg {
 #define USV_PAIR_SPLIT_R 7  // radius from which the row's entries are read in two batches
 #endif
     static constexpr int SPLIT = RAD >= USV_PAIR_SPLIT_R ? 2 : 1;
+    // Chain jump: the row sums H[x] = A[x + WIN] - A[x] (x < K) read the prefix A only at 0..K-1 and
+    // WIN..WIN+K-1, so the WIN - K + 1 increments j = K-1 .. WIN-1 between them are folded into quads:
+    // one 4-byte v_sad_u8 (+ v_sad_hi_u8) per 4 columns, the R bytes packed from the staged entries
+    // (r = 5: 18 -> 15 chain steps, r = 7: 22 -> 16).
+#ifndef USV_PAIR_JUMP
+#define USV_PAIR_JUMP 1
+#endif
+    static constexpr int JA = K - 1;                                  // first increment in a quad
+    static constexpr int JN = USV_PAIR_JUMP ? (WIN - K + 1) / 4 : 0;  // quads
+    static constexpr int JE = JA + 4 * JN;                            // singles resume here
     static constexpr int PD = USV_PAIR_PD > 0 && USV_PAIR_PD < NB ? USV_PAIR_PD : NB - 1;
     static constexpr int KRB = WIN;
     static constexpr int RBUF_OFF = 0;
@@ -216,19 +226,39 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
         }
         uint32_t Lv[NPOS];
+        uint32_t Lw[8];
         {
             wait_lgkm0_pin<LS::NLD>(lw_next);
             LWords cur = lw_next;
-            uint32_t lw[8];
-            unpack_words<LS::NLD>(cur, lw);
+            unpack_words<LS::NLD>(cur, Lw);
 #pragma unroll
             for (int j = 0; j < NPOS; ++j) {
                 const int bidx = LS::byte(j);
-                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = lw[bidx >> 2];
-                else Lv[j] = (lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = Lw[bidx >> 2];
+                else Lv[j] = (Lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
         auto lbyte = [&](int j) -> uint32_t { return Lv[j]; };
+        // the 4 L bytes of quad increments j .. j + 3 as one dword (one funnel shift of two segment words when
+        // the bytes are consecutive, i.e. interior tiles; the border tiles' replicated bytes are or-ed)
+        auto lquad = [&](auto jt) -> uint32_t {
+            constexpr int j = decltype(jt)::value;
+            constexpr int b0 = LS::byte(j);
+            constexpr bool consec = LS::byte(j + 1) == b0 + 1 && LS::byte(j + 2) == b0 + 2 && LS::byte(j + 3) == b0 + 3;
+            if constexpr (consec && (b0 & 3) == 0) {
+                return Lw[b0 >> 2];
+            } else if constexpr (consec) {
+                return (uint32_t)((((uint64_t)Lw[(b0 >> 2) + 1] << 32) | Lw[b0 >> 2]) >> (8 * (b0 & 3)));
+            } else {
+                uint32_t v = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int b = LS::byte(j + i);
+                    v |= ((Lw[b >> 2] >> (8 * (b & 3))) & 0xFFu) << (8 * i);
+                }
+                return v;
+            }
+        };
         using VT = typename VecT<C::VEC>::T;
         int boff = C::STATIC ? I * C::NRS : slot_of(t) * C::NRS;
         if constexpr (!C::STATIC) asm volatile("" : "+s"(boff));
@@ -276,15 +306,31 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         // fenced: the two independent dependency chains interleave instruction by instruction.
         uint32_t A[NPOS + 1];
         A[0] = 0;
+        // op at increment j: a single step (A[j + 1]), the first increment of a quad (A[j + 4]), or an
+        // increment folded into the quad before it (no op; its argmin piece still follows here)
+        constexpr auto is_quad = [](int j) { return j >= C::JA && j < C::JE && (j - C::JA) % 4 == 0; };
+        constexpr auto is_op = [](int j) { return j < C::JA || j >= C::JE || (j - C::JA) % 4 == 0; };
+        // highest staged entry the ops up to increment j read (single j: j + 1; quad at j: j + 4)
+        constexpr auto need = [is_quad, is_op](int j) {
+            int n = 0;
+            for (int i = 0; i <= j; ++i)
+                if (is_op(i)) n = is_quad(i) ? i + 4 : i + 1;
+            return n;
+        };
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
-            // first step that needs pair k0; pairs are retired USV_PAIR_RDASM_GRP at a time (a group never spans
-            // the two read batches of r = 7)
-            constexpr int k0 = (j + 1) / 2, GRP = USV_PAIR_RDASM_GRP;
-            constexpr int bstart = k0 < NV1 ? 0 : NV1, bend = k0 < NV1 ? NV1 : NV;
-            if constexpr (RDASM && (j == 0 || (j & 1)) && (k0 - bstart) % GRP == 0) {
-                constexpr int k1 = k0 + GRP < bend ? k0 + GRP : bend;  // pairs [k0, k1)
-                constexpr int later = bend - k1;                        // reads of its batch issued after them
+            // the pairs this op needs that no earlier op waited for; retired USV_PAIR_RDASM_GRP at a time
+            // (a group never spans the two read batches of r = 7)
+            constexpr int GRP = USV_PAIR_RDASM_GRP;
+            constexpr int kp = j == 0 ? -1 : need(j - 1) / 2;  // pairs [0, kp] already retired
+            constexpr int kn = need(j) / 2;                    // pairs [0, kn] needed now
+            if constexpr (RDASM && is_op(j) && kn > kp) {
+                constexpr int k0 = kp + 1;
+                constexpr int bstart = k0 < NV1 ? 0 : NV1, bend = k0 < NV1 ? NV1 : NV;
+                constexpr int kg = ((kn - bstart) / GRP + 1) * GRP + bstart;  // whole groups up to kn
+                constexpr int k1 = kg < bend ? kg : bend;                      // pairs [k0, k1)
+                constexpr int later = bend - k1;                               // reads of its batch issued after them
+                static_assert(kn < bend, "an op's pairs lie in one read batch");
                 // lgkmcnt(later), vmcnt / expcnt left at their maxima; the scheduling barriers keep the
                 // pairs' uses below the wait (the compiler believes the asm outputs ready at once)
                 __builtin_amdgcn_sched_barrier(0);
@@ -300,8 +346,20 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                     E[2 * k + 1] = ev[k].y;
                 }
             }
-            const uint32_t l = lbyte(j);
-            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            if constexpr (is_quad(j)) {
+                // four increments in one step: lo (d) |L_{j+i} - E[j+i+1]|, hi (d + 1) |L_{j+i} - E[j+i]|,
+                // i = 0..3; the entries are zero-extended bytes, packed here by four v_perm (m = bytes of
+                // E[j+1..j+3], then E[j] below it for hi and E[j+4] above it for lo)
+                const uint32_t t = __builtin_amdgcn_perm(E[j + 2], E[j + 1], 0x0c0c0400u);
+                const uint32_t m = __builtin_amdgcn_perm(E[j + 3], t, 0x0c040100u);
+                const uint32_t r_hi = __builtin_amdgcn_perm(m, E[j], 0x06050400u);
+                const uint32_t r_lo = __builtin_amdgcn_perm(E[j + 4], m, 0x04020100u);
+                const uint32_t l4 = lquad(jt);
+                A[j + 4] = __builtin_amdgcn_sad_hi_u8(l4, r_hi, __builtin_amdgcn_sad_u8(l4, r_lo, A[j]));
+            } else if constexpr (is_op(j)) {
+                const uint32_t l = lbyte(j);
+                A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            }
             pre(jt);
             if constexpr (EARLY_SUB) __builtin_amdgcn_sched_barrier(0);
         };
@@ -323,9 +381,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #pragma unroll
                 for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
             }
-#pragma unroll
-            for (int j = J1; j < NPOS; ++j)
-                A[j + 1] = __builtin_amdgcn_sad_hi_u8(lbyte(j), E[j], __builtin_amdgcn_sad_u8(lbyte(j), E[j + 1], A[j]));
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (chain_step(std::integral_constant<int, J1 + J>{}), ...);
+            }(std::make_integer_sequence<int, NPOS - J1>{});
         }
 #pragma unroll
         for (int x = 0; x < K; ++x) {
