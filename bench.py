@@ -745,7 +745,14 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     Lc, Rc = Lt[:, :1918], Rt[:, :1918]
     ssd = StereoBlockMatcher(D, w, "ssd", kernel="fast")
     us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s, preload="self")
-    out["ssd_fast"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6)}
+    out["ssd_fast"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6),
+                       "kernel": "ssd_fast_kernel (VALU)"}
+    # the window cross term on the matrix cores (csrc/usv_ssd_mfma.hip): what AUTO runs for this SSD shape
+    ssd = StereoBlockMatcher(D, w, "ssd", kernel="matrix")
+    us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s, preload="self")
+    out["ssd_matrix"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6),
+                         "kernel": "ssd_mfma_kernel (v_mfma_i32_32x32x32_i8)",
+                         "mfma_tops": 2.0 * 32 * 32 * 32 * (60 * H * ((W + 63) // 64)) / (us * 1e-6) / 1e12}
     for kernel, n in (("tiled", steps * 8), ("generic", steps)):
         ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)
         us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s, preload="self")
@@ -754,9 +761,11 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
         us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s, preload="self")
         out[f"sad_{kernel}_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
                                       "value": 1918 * H / (us * 1e-6)}
-    out["note"] = "AUTO runs ssd_fast for SSD at 11 <= w <= 15 and the tiled kernel (vertical running sums, " \
-                  "LDS-DMA row ring) for other SSD windows and for shapes outside the fast kernels (W % 4, W < 48, " \
-                  "unaligned pitch or base); generic = one thread per pixel, direct window, only for w > 31"
+    out["note"] = "AUTO runs ssd_matrix for SSD at w <= 11 and D = 32..160 step 32, ssd_fast at 11 <= w <= 15 " \
+                  "otherwise, and the tiled kernel (vertical running sums, LDS-DMA row ring) for other SSD windows " \
+                  "and for shapes outside the fast kernels (W % 4, W < 48, unaligned pitch or base); generic = one " \
+                  "thread per pixel, direct window, only for w > 31; mfma_tops counts the 60 MFMAs per 64-column " \
+                  "tile-row the matrix kernel issues at D = 128 (padding included)"
     return out
 
 

@@ -1,0 +1,112 @@
+"""GPU parity of the matrix-core SSD kernel (csrc/usv_ssd_mfma.hip, kernel="matrix") against the CPU oracle.
+
+The kernel computes the window cross term Σ a'b' with v_mfma_i32_32x32x32_i8 and the argmin over SB - 2C
+(SSD variant; oracle/sad_oracle.c).  Integer arithmetic, so the disparity maps must be
+bit-identical to the oracle's, ties (smallest d) and replicate borders included, and the fused distance map
+bit-identical to the table gather.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle_lib import oracle_sad
+from unsynchronized_stereo_vision_proj325_amd import StereoBlockMatcher, _lib
+from unsynchronized_stereo_vision_proj325_amd.engine import distance_lut_cm
+from unsynchronized_stereo_vision_proj325_amd.synthetic import synthetic_pair
+
+pytestmark = pytest.mark.gpu
+THREADS = 16
+
+
+def _mismatch(a, b):
+    bad = np.argwhere(a != b)
+    return f"{len(bad)} mismatches, first at {bad[:5].tolist()}" if len(bad) else ""
+
+
+def _run(dev, L, R, D, w, kernel="matrix", with_distance=False):
+    Lt = torch.from_numpy(np.ascontiguousarray(L)).to(dev)
+    Rt = torch.from_numpy(np.ascontiguousarray(R)).to(dev)
+    out = StereoBlockMatcher(D, w, "ssd", kernel=kernel).compute(Lt, Rt, with_distance=with_distance)
+    torch.cuda.synchronize()
+    return (out[0].cpu().numpy(), out[1].cpu().numpy()) if with_distance else out.cpu().numpy()
+
+
+def test_matrix_ssd_config_c_full_size(gpu):
+    """The headline shape (1920x1080, 11x11, D = 128) with the fused distance map; AUTO takes the same kernel."""
+    L, R, _ = synthetic_pair(1920, 1080, 128, pair_index=5, noise=2)
+    ref = oracle_sad(L, R, 128, 11, "ssd", "sliding", threads=THREADS)
+    got, dist = _run(gpu, L, R, 128, 11, with_distance=True)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    assert np.array_equal(dist, distance_lut_cm("moving_object")[ref])
+    auto = _run(gpu, L, R, 128, 11, kernel="auto")
+    assert np.array_equal(auto, ref), _mismatch(auto, ref)
+
+
+@pytest.mark.parametrize("W,H,D,w", [(64, 16, 32, 3), (65, 20, 64, 5), (200, 77, 96, 7), (333, 41, 128, 9),
+                                     (1000, 50, 160, 11), (128, 300, 128, 11), (96, 9, 32, 11), (130, 33, 160, 3)])
+def test_matrix_ssd_shapes(gpu, W, H, D, w):
+    """Every window 3..11 and D = 32..160: border tiles (the first m-blocks left of column 0, the last tile shifted
+    to W - 64 and overlapping its neighbour), bands of a few rows, frames barely one tile wide."""
+    rng = np.random.default_rng(W * 31 + H * 7 + D + w)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    ref = oracle_sad(L, R, D, w, "ssd", "sliding", threads=THREADS)
+    got = _run(gpu, L, R, D, w)
+    assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
+
+
+@pytest.mark.parametrize("levels", [2, 4, 64])
+def test_matrix_ssd_ties(gpu, levels):
+    """Low-entropy images (2, 4 or 64 grey levels): many equal costs, the smallest d must win every tie."""
+    rng = np.random.default_rng(levels)
+    W, H, D, w = 256, 40, 128, 11
+    L = (rng.integers(0, levels, (H, W)) * (255 // max(levels - 1, 1))).astype(np.uint8)
+    R = (rng.integers(0, levels, (H, W)) * (255 // max(levels - 1, 1))).astype(np.uint8)
+    ref = oracle_sad(L, R, D, w, "ssd", "naive")
+    got = _run(gpu, L, R, D, w)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+
+
+def test_matrix_ssd_extreme_costs(gpu):
+    """0 against 255 (the largest SSD, 121 x 255^2): the i32 keys must not wrap; all-tie and constant images."""
+    H, W, D, w = 40, 192, 96, 11
+    L = np.zeros((H, W), dtype=np.uint8)
+    R = np.full((H, W), 255, dtype=np.uint8)
+    R[:, ::7] = 0
+    assert np.array_equal(_run(gpu, L, R, D, w), oracle_sad(L, R, D, w, "ssd", "naive"))
+    R[:] = 255
+    assert np.array_equal(_run(gpu, L, R, D, w), oracle_sad(L, R, D, w, "ssd", "naive"))
+    L[:] = 255
+    R[:] = 0
+    assert np.array_equal(_run(gpu, L, R, D, w), oracle_sad(L, R, D, w, "ssd", "naive"))
+    L[:] = 7
+    R[:] = 7
+    assert np.array_equal(_run(gpu, L, R, D, w), np.zeros((H, W), dtype=np.uint8))
+
+
+def test_matrix_ssd_pitched_unaligned_and_batched(gpu):
+    """Rows with a pitch wider than W and an odd base offset (byte loads: any alignment), and a batch of three
+    pairs through the batch entry point (AUTO -> the matrix kernel)."""
+    rng = np.random.default_rng(11)
+    H, W, D, w = 70, 300, 64, 9
+    big_l = torch.from_numpy(rng.integers(0, 256, (H, W + 13), dtype=np.uint8)).to(gpu)
+    big_r = torch.from_numpy(rng.integers(0, 256, (H, W + 13), dtype=np.uint8)).to(gpu)
+    Lv, Rv = big_l[:, 3:3 + W], big_r[:, 3:3 + W]
+    got = StereoBlockMatcher(D, w, "ssd", kernel="matrix").compute(Lv, Rv).cpu().numpy()
+    ref = oracle_sad(Lv.cpu().numpy(), Rv.cpu().numpy(), D, w, "ssd", "sliding", threads=THREADS)
+    assert np.array_equal(got, ref), _mismatch(got, ref)
+    pairs = [synthetic_pair(256, 48, 96, pair_index=i, noise=2)[:2] for i in range(3)]
+    Lb = torch.from_numpy(np.stack([p[0] for p in pairs])).to(gpu)
+    Rb = torch.from_numpy(np.stack([p[1] for p in pairs])).to(gpu)
+    out = StereoBlockMatcher(96, 11, "ssd").compute(Lb, Rb).cpu().numpy()
+    for i, (L, R) in enumerate(pairs):
+        ref = oracle_sad(L, R, 96, 11, "ssd", "sliding", threads=THREADS)
+        assert np.array_equal(out[i], ref), (i, _mismatch(out[i], ref))
+
+
+@pytest.mark.parametrize("W,H,D,w", [(128, 16, 100, 11), (128, 16, 192, 11), (128, 16, 64, 13), (60, 16, 32, 5)])
+def test_matrix_ssd_refuses_unsupported(gpu, W, H, D, w):
+    """Outside w <= 11, D in 32..160 step 32, W >= 64 the selector refuses (AUTO falls back to the VALU kernels)."""
+    L = torch.zeros((H, W), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.UsvError):
+        StereoBlockMatcher(D, w, "ssd", kernel="matrix").compute(L, L)

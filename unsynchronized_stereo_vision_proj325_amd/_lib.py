@@ -32,7 +32,7 @@ STATUS_NAMES = {
 
 METRIC_SAD, METRIC_SSD = 0, 1
 DIST_MOVING_OBJECT, DIST_CANNY = 0, 1
-KERNEL_AUTO, KERNEL_FAST, KERNEL_GENERIC, KERNEL_TILED = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_FAST, KERNEL_GENERIC, KERNEL_TILED, KERNEL_MATRIX = 0, 1, 2, 3, 4
 STREAM_DEVICE_DIST = 1
 
 

@@ -111,16 +111,19 @@ usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
     usv_status st = validate(a);
     if (st != USV_OK) return st;
     if (kernel != USV_KERNEL_AUTO && kernel != USV_KERNEL_FAST && kernel != USV_KERNEL_GENERIC &&
-        kernel != USV_KERNEL_TILED)
+        kernel != USV_KERNEL_TILED && kernel != USV_KERNEL_MATRIX)
         return USV_ERR_INVALID_ARG;
     if (kernel == USV_KERNEL_FAST && !usv::fast_path_supported(a)) return USV_ERR_UNSUPPORTED;
     if (kernel == USV_KERNEL_TILED && !usv::tiled_path_supported(a)) return USV_ERR_UNSUPPORTED;
+    if (kernel == USV_KERNEL_MATRIX && !usv::ssd_mfma_supported(a)) return USV_ERR_UNSUPPORTED;
     if (a.dist && (st = resolve_lut(a.lut, &a.lut)) != USV_OK) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (kernel) {
         case USV_KERNEL_AUTO:
-            // fast SAD kernels, else the tiled sliding-window kernel (SSD, any shape, w <= 31),
-            // else the direct-window kernel (w > 31, or a window too large for the tiled ring)
+            // SSD on the matrix cores where supported, else the fast kernels, else the tiled sliding-window
+            // kernel (any shape, w <= 31), else the direct-window kernel (w > 31, or a window too large for the
+            // tiled ring)
+            if (usv::ssd_mfma_supported(a)) return to_status(usv::launch_ssd_mfma(a, s));
             if (usv::fast_path_supported(a)) return to_status(usv::launch_fast(a, s));
             if (usv::tiled_path_supported(a)) return to_status(usv::launch_tiled(a, s));
             return to_status(usv::launch_generic(a, s));
@@ -131,6 +134,8 @@ usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
             return to_status(usv::launch_tiled(a, s));
         case USV_KERNEL_GENERIC:
             return to_status(usv::launch_generic(a, s));
+        case USV_KERNEL_MATRIX:
+            return to_status(usv::launch_ssd_mfma(a, s));
         default:
             return USV_ERR_INVALID_ARG;
     }

@@ -65,6 +65,11 @@ hipError_t launch_pair(const MatchArgs& a, hipStream_t s);
 // SSD kernel (usv_sad_ssd.hip): 11 <= w <= 15, on shapes fast_path_supported accepts.
 hipError_t launch_ssd(const MatchArgs& a, hipStream_t s);
 
+// SSD with the window cross term on the matrix cores (usv_ssd_mfma.hip): w = 3 .. 11, D = 32 .. 192 in steps of
+// 32, W >= 64, any pitch / alignment.  hipErrorInvalidValue otherwise.
+bool ssd_mfma_supported(const MatchArgs& a);
+hipError_t launch_ssd_mfma(const MatchArgs& a, hipStream_t s);
+
 // Grouped paired-disparity kernel for small disparity ranges (usv_sad_group.hip): SAD, even
 // 16 < D <= 64, 5 <= w <= 9, on shapes fast_path_supported accepts.  hipErrorInvalidValue otherwise.
 bool group_path_supported(const MatchArgs& a);

@@ -196,13 +196,13 @@ __global__ __launch_bounds__(kPT) void hsv_hist_kernel(HistJob j0, HistJob j1, i
     }
 }
 
-// Quads per thread of the V-histogram pass: it only reads, so four quads' loads in flight per thread and half
-// the blocks (half the per-block LDS clears, barriers and bin flushes) -- a stand-alone probe of this pass at
-// 1080p ran 4.38 us at two quads per thread, 3.68 at four, 3.94 at eight, with a no-histogram floor of
-// 3.37 us at four (scripts/probes/hist_probe.hip, profiles/probes_r05/hist_probe_r05.txt): the LDS atomics are
-// not what binds it; interleaving copies over the banks (32 or 64 per block) was slower.
+// Quads per thread of the V-histogram pass.  A stand-alone probe of the pass at 1080p (scripts/probes/hist_probe.hip,
+// profiles/probes_r05/hist_probe_r05.txt) ran 4.38 us at two quads per thread, 3.68 at four, 3.94 at eight,
+// with a no-histogram floor of 3.37 us at four: the LDS atomics are not what binds it, and interleaving copies
+// over the banks (32 or 64 per block) was slower.  In the product kernel four quads per thread measured slower
+// than two (rocprof 8.3 vs 6.3 us average, 5.9 vs 4.1 us minimum, profiles/r05e vs r05a), so two it stays.
 #ifndef USV_HIST_KU
-#define USV_HIST_KU 4
+#define USV_HIST_KU 2
 #endif
 constexpr int kUHist = USV_HIST_KU;
 

@@ -1,0 +1,288 @@
+// usv_ssd_mfma.hip -- SSD block match with the window's cross term on the gfx950 matrix cores
+// (ssd_mfma_kernel: v_mfma_i32_32x32x32_i8; w <= 11, D a multiple of 32 up to 160).
+//
+// Spec: SURVEY.md §8(a) A1, SSD variant (restated in oracle/sad_oracle.c).  With a' = a - 128 and b' = b - 128
+// (signed bytes, exact: a' = (int8)(a ^ 0x80)), for output pixel x, disparity d and R window centre m = x - d:
+//   cost(x, d) = Σ (a - b)^2 = SA(x) + SB(m) - 2 C(m, x),
+//   SA(x) = Σ a'^2, SB(m) = Σ b'^2 and C(m, x) = Σ a' b' over the w x w window (replicate border).
+// SA is the same for every d of a pixel, so the argmin over d is the argmin of SB(m) - 2 C(m, x), and C is a
+// matrix product over k = (window row, window column):
+//   C[m][x] = Σ_k A[m][k] B[k][x],   A[m][k] = b'(row, m - r + dx),   B[k][x] = a'(row, x - r + dx).
+//
+// Operands come from COLUMN RECORDS: the LDS holds, per staged column, 16 bytes = the column's value in the 16
+// slots of a row ring (row ρ in byte ρ & 15), holding exactly the current window's rows and zero elsewhere (a row
+// is written when it enters the window and zeroed when it leaves).  A K-step of v_mfma_i32_32x32x32_i8 is then two
+// window columns (dx = 2 s + h for lane half h) x the 16 ring slots: lane (i, h) of the A operand is the record of
+// R column m_i - r + dx, lane (j, h) of B the record of L column x_j - r + dx -- one aligned ds_read_b128 each,
+// the same byte order (ring slot) in both, so the k order inside a step is the same permutation of window rows
+// for A and B, which the sum does not see (profiles/probes_r05/mfma_i8_layout_r05.txt: any consistent k order
+// gives the product).  dx >= w reads a zero record.  Unaligned LDS reads are exact on gfx950 but serialise
+// (255 vs 39 cycles per wave-instruction, profiles/probes_r05/lds_unaligned_r05.txt): records keep every read
+// 16-byte aligned, and the ring needs no im2col copy per output row.
+//
+// A wave owns XT = 64 output columns (two 32-column sub-tiles t) and a band of rows.  Sub-tile t's R centres run
+// over m-blocks b = t .. t + D/32 of the wave's NBM = 2 + D/32 blocks of 32 from m_lo = x0 - D; block b = t holds
+// d = D + j - i (valid for j < i), block t + D/32 holds d = j - i (valid for j >= i), the blocks between are all
+// valid (i: the block's m row, j: the sub-tile's x column).  Per output row:
+//   * stage: the window's new row enters the R / L records (one byte per record), the row that left is zeroed;
+//   * SB: V(c) = Σ b'^2 of R column c's record (four v_dot4_i32_i8), an exclusive wave prefix X of V, then
+//     SB(m) = X(n + w) - X(n) for n = m - m_lo, and the key table -T(n), T(n) = (SB << 8) + 255 - n, in LDS;
+//   * B operands for both sub-tiles and every K-step; per m-block the A operands of its K-steps, the MFMAs of the
+//     sub-tiles it serves and the epilogue: -key = 512 C - T(n) (one v_lshl_add_u32 per product, the MFMA writing
+//     VGPRs: -amdgpu-mfma-vgpr-form), invalid d masked in the two edge blocks, a running max per sub-tile;
+//   * key = (SB - 2C) * 256 + 255 - n: the minimum is the smallest cost, ties -> the largest m = the smallest d
+//     (the SAD kernels' rule); |SB - 2C| * 256 < 2^31 for w <= 11.
+// The C/D layout is column = lane & 31 (x), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (m): the reduction over m
+// stays in the lane's registers; one half-wave swap at the end.  Integer arithmetic: bit-exact with the oracle.
+#include <algorithm>
+
+#include "usv_sad_common.hpp"
+
+namespace usv {
+namespace {
+
+typedef int mi32x4 __attribute__((ext_vector_type(4)));
+typedef int mi32x16 __attribute__((ext_vector_type(16)));
+
+template <int RAD, int DB>
+struct MCfg {
+    static constexpr int WIN = 2 * RAD + 1;
+    static constexpr int NS = 2;              // 32-column sub-tiles per wave
+    static constexpr int XT = 32 * NS;        // output columns per wave
+    static constexpr int NBM = NS + DB;       // 32-row m-blocks
+    static constexpr int NM = 32 * NBM;       // R window centres per tile
+    static constexpr int NSTEP = RAD + 1;     // K-steps: window columns 2 s, 2 s + 1 (column w reads zeros)
+    static constexpr int NRC = 256;           // R records (columns rs .. rs + 255; NM + 16 are read)
+    static constexpr int NLC = 128;           // L records (XT + 16 are read)
+    static constexpr int R_OFF = 0;
+    static constexpr int L_OFF = R_OFF + 16 * NRC;
+    static constexpr int Z_OFF = L_OFF + 16 * NLC;       // one zero record
+    static constexpr int X_OFF = Z_OFF + 16;             // exclusive prefix of V (256 i32)
+    static constexpr int T_OFF = X_OFF + 4 * 256;        // key table T(n) (NM i32)
+    static constexpr int LUT_OFF = T_OFF + 4 * 256;      // distance table (256 f64)
+    static constexpr int SMEM = LUT_OFF + 8 * 256;
+    static_assert(WIN <= 11, "|SB - 2C| * 256 fits an i32 key for w <= 11");
+    static_assert(NM <= 256, "key low byte: 255 - n");
+    static_assert(NM + 16 <= NRC && XT + 16 <= NLC && NRC == 256 && NLC == 128, "records: 4 / 2 per lane");
+    static_assert(WIN <= 15, "the window's rows and the one leaving fit the 16-slot ring");
+};
+
+// lanes whose C row of register r lies below their column index: (lane & 31) < (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+__host__ __device__ constexpr uint64_t row_gt_col_mask(int r) {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l)
+        if ((l & 31) < (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) m |= 1ull << l;
+    return m;
+}
+
+template <int RAD, int DB>
+__global__ __launch_bounds__(64) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
+                                                      uint8_t* __restrict__ disp, double* __restrict__ dist,
+                                                      MatchArgs a, int n_xt, int bands) {
+    using C = MCfg<RAD, DB>;
+    constexpr int WIN = C::WIN, NS = C::NS, XT = C::XT, NBM = C::NBM, NSTEP = C::NSTEP, D = 32 * DB;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[C::SMEM];
+    const int l = threadIdx.x, j = l & 31, h = l >> 5;
+    int blk = blockIdx.x;
+    const int xt = blk % n_xt;
+    blk /= n_xt;
+    const int band = blk % bands;
+    const int pair = blk / bands;
+    const int x0 = min(xt * XT, a.W - XT);
+    const int y_begin = (int)((long long)a.H * band / bands), y_end = (int)((long long)a.H * (band + 1) / bands);
+    if (y_end <= y_begin) return;
+    const uint8_t* L = Lg + (size_t)pair * a.pair_stride;
+    const uint8_t* R = Rg + (size_t)pair * a.pair_stride;
+    disp += (size_t)pair * a.disp_stride;
+    if (dist) dist += (size_t)pair * a.dist_stride;
+    const int m_lo = x0 - D;
+    const int rs = m_lo - RAD, ls = x0 - RAD;  // first R / L record's column
+    const __amdgpu_buffer_rsrc_t rsrcL =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(L), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(R), (short)0, 0x7FFFFFFF, 0x00020000);
+
+    // every record starts empty (zero); the zero record; the distance table
+    for (int i = l; i < (C::X_OFF) / 16; i += 64) reinterpret_cast<mi32x4*>(smem)[i] = mi32x4{0, 0, 0, 0};
+    if (dist)
+        for (int i = l; i < 256; i += 64) reinterpret_cast<double*>(smem + C::LUT_OFF)[i] = a.lut[i];
+
+    // row rho's staged bytes, lane l: R columns rs + l + 64 q (q < 4; records l + 64 q) and L columns
+    // ls + l + 64 q (q < 2), clamped to the image (replicate border).  Strided records keep the byte stores of
+    // one instruction on 8 banks per 32 lanes (4-way) where records 4l .. 4l+3 per lane would put them on 2.
+    auto load_row = [&](int rho, uint32_t (&vr)[4], uint32_t (&vl)[2]) {
+        const int y = min(max(rho, 0), a.H - 1);
+        const uint32_t base = (uint32_t)(y * a.pitch);
+        const int Wm1 = a.W - 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            vr[q] = l + 64 * q < C::NM + 16
+                        ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcR, base + (uint32_t)min(max(rs + l + 64 * q, 0), Wm1), 0, 0)
+                        : 0x80u;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            vl[q] = l + 64 * q < XT + 16
+                        ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcL, base + (uint32_t)min(max(ls + l + 64 * q, 0), Wm1), 0, 0)
+                        : 0x80u;
+    };
+    // row rho's bytes (XOR 0x80: signed) into ring slot rho & 15 of the lane's records; 0x80 clears the slot of a
+    // row that left the window
+    auto put_row = [&](int rho, const uint32_t (&vr)[4], const uint32_t (&vl)[2]) {
+        const int slot = rho & 15;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) smem[C::R_OFF + 16 * (l + 64 * q) + slot] = (uint8_t)(vr[q] ^ 0x80u);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) smem[C::L_OFF + 16 * (l + 64 * q) + slot] = (uint8_t)(vl[q] ^ 0x80u);
+    };
+    const uint32_t kClearR[4] = {0x80u, 0x80u, 0x80u, 0x80u}, kClearL[2] = {0x80u, 0x80u};
+
+    // prologue: window rows y_begin - r .. y_begin + r - 1
+    for (int rho = y_begin - RAD; rho < y_begin + RAD; ++rho) {
+        uint32_t vr[4], vl[2];
+        load_row(rho, vr, vl);
+        put_row(rho, vr, vl);
+    }
+    uint32_t pr[4], pl[2];  // the next entering row's bytes, loaded one row ahead
+    load_row(y_begin + RAD, pr, pl);
+    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
+    const mi32x4* recR = reinterpret_cast<const mi32x4*>(smem + C::R_OFF);
+    const mi32x4* recL = reinterpret_cast<const mi32x4*>(smem + C::L_OFF);
+
+    for (int y = y_begin; y < y_end; ++y) {
+        // the window's new row y + r enters, the row y - r - 1 left (its slot is cleared); fetch the next one
+        if (y > y_begin) put_row(y - RAD - 1, kClearR, kClearL);
+        put_row(y + RAD, pr, pl);
+        if (y + 1 < y_end) load_row(y + 1 + RAD, pr, pl);
+
+        // V(c) = Σ b'^2 over the window (R record c), X = its exclusive prefix, T(n) for the tile's NM centres
+        {
+            int v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const mi32x4 rc = recR[4 * l + e];
+                int s = 0;
+                s = __builtin_amdgcn_sdot4(rc.x, rc.x, s, false);
+                s = __builtin_amdgcn_sdot4(rc.y, rc.y, s, false);
+                s = __builtin_amdgcn_sdot4(rc.z, rc.z, s, false);
+                s = __builtin_amdgcn_sdot4(rc.w, rc.w, s, false);
+                v[e] = s;
+            }
+            const int p1 = v[0] + v[1], p2 = p1 + v[2], tot = p2 + v[3];
+            int incl = tot;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off, 64);
+                if (l >= off) incl += t;
+            }
+            const int ex = incl - tot;
+            reinterpret_cast<mi32x4*>(smem + C::X_OFF)[l] = mi32x4{ex, ex + v[0], ex + p1, ex + p2};
+            const int* X = reinterpret_cast<const int*>(smem + C::X_OFF);
+            int* T = reinterpret_cast<int*>(smem + C::T_OFF);
+#pragma unroll
+            for (int n = l; n < C::NM; n += 64) T[n] = n - 255 - ((X[n + WIN] - X[n]) << 8);  // -T(n)
+        }
+        // B operands (L records): sub-tile t, K-step s -> window column dx = 2 s + h of output column x0 + 32 t + j
+        mi32x4 Bop[NS][NSTEP];
+#pragma unroll
+        for (int s = 0; s < NSTEP; ++s) {
+            const int dx = 2 * s + h;
+#pragma unroll
+            for (int t = 0; t < NS; ++t)
+                Bop[t][s] = dx < WIN ? recL[32 * t + j + dx] : *reinterpret_cast<const mi32x4*>(smem + C::Z_OFF);
+        }
+        int run[NS];  // running max of -key
+#pragma unroll
+        for (int t = 0; t < NS; ++t) run[t] = (int)0x80000000u;
+#pragma unroll
+        for (int b = 0; b < NBM; ++b) {
+            mi32x4 Aop[NSTEP];
+#pragma unroll
+            for (int s = 0; s < NSTEP; ++s) Aop[s] = recR[32 * b + j + 2 * s + h];
+            const mi32x4* Tb = reinterpret_cast<const mi32x4*>(smem + C::T_OFF + 4 * (32 * b + 4 * h));
+            mi32x4 Tv[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Tv[g] = Tb[2 * g];  // rows 8 g + 4 h .. + 3 of the block
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                if (b < t || b > t + DB) continue;
+                mi32x16 acc = {};
+#pragma unroll
+                for (int s = 0; s < NSTEP; ++s)
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aop[s], Bop[t][s], acc, 0, 0, 0);
+                int k[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) k[r] = (acc[r] << 9) + Tv[r >> 2][r & 3];  // -key: one v_lshl_add_u32
+                if (b == t) {  // d = D + j - i: valid for j < i
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) k[r] = (int)sel_mask(0x80000000u, (uint32_t)k[r], row_gt_col_mask(r));
+                } else if (b == t + DB) {  // d = j - i: valid for j >= i
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) k[r] = (int)sel_mask((uint32_t)k[r], 0x80000000u, row_gt_col_mask(r));
+                }
+                int m = run[t];
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) m = max(max(m, k[r]), k[r + 1]);
+                run[t] = m;
+            }
+        }
+        // a column's rows are split over the two half-waves: combine; lane (j, h) writes sub-tile h's column j
+#pragma unroll
+        for (int t = 0; t < NS; ++t) run[t] = max(run[t], __shfl_xor(run[t], 32, 64));
+        const int key = -(int)sel_mask((uint32_t)run[0], (uint32_t)run[1], 0xFFFFFFFF00000000ull);
+        const int d = 32 * h + j + D - 255 + (key & 0xFF);
+        const int x = x0 + 32 * h + j;
+        disp[(size_t)y * a.disp_pitch + x] = (uint8_t)d;
+        if (dist) dist[(size_t)y * a.dist_pitch + x] = lut_s[d];
+    }
+}
+
+template <int RAD, int DB>
+hipError_t launch_mfma_rd(const MatchArgs& a, hipStream_t s) {
+    using C = MCfg<RAD, DB>;
+    const int n_xt = (a.W + C::XT - 1) / C::XT;
+#ifndef USV_SSD_MFMA_WAVES
+#define USV_SSD_MFMA_WAVES 8  // target resident waves per CU (one-wave workgroups)
+#endif
+    const long target = (long)cu_count() * USV_SSD_MFMA_WAVES;
+    long bands = (target + (long)n_xt * a.batch - 1) / ((long)n_xt * a.batch);
+    bands = std::max(1L, std::min(bands, (long)std::max(1, a.H / 4)));
+    const long total = (long)n_xt * bands * a.batch;
+    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((ssd_mfma_kernel<RAD, DB>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a,
+                       n_xt, (int)bands);
+    return hipGetLastError();
+}
+
+template <int RAD>
+hipError_t launch_mfma_r(const MatchArgs& a, hipStream_t s) {
+    switch (a.D / 32) {
+        case 1: return launch_mfma_rd<RAD, 1>(a, s);
+        case 2: return launch_mfma_rd<RAD, 2>(a, s);
+        case 3: return launch_mfma_rd<RAD, 3>(a, s);
+        case 4: return launch_mfma_rd<RAD, 4>(a, s);
+        case 5: return launch_mfma_rd<RAD, 5>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+bool ssd_mfma_supported(const MatchArgs& a) {
+    // SSD, w = 3 .. 11, D = 32 .. 160 in steps of 32, at least one 64-column tile, 32-bit row offsets
+    return a.metric == 1 && (a.w & 1) && a.w >= 3 && a.w <= 11 && a.D % 32 == 0 && a.D >= 32 && a.D <= 160 &&
+           a.W >= 64 && (long long)a.pitch * a.H < (1LL << 31);
+}
+
+hipError_t launch_ssd_mfma(const MatchArgs& a, hipStream_t s) {
+    if (!ssd_mfma_supported(a)) return hipErrorInvalidValue;
+    switch ((a.w - 1) / 2) {
+        case 1: return launch_mfma_r<1>(a, s);
+        case 2: return launch_mfma_r<2>(a, s);
+        case 3: return launch_mfma_r<3>(a, s);
+        case 4: return launch_mfma_r<4>(a, s);
+        case 5: return launch_mfma_r<5>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace usv

@@ -22,7 +22,7 @@ from . import _lib
 _METRICS = {"sad": _lib.METRIC_SAD, "ssd": _lib.METRIC_SSD}
 _MODELS = {"moving_object": _lib.DIST_MOVING_OBJECT, "canny": _lib.DIST_CANNY}
 _KERNELS = {"auto": _lib.KERNEL_AUTO, "fast": _lib.KERNEL_FAST, "generic": _lib.KERNEL_GENERIC,
-            "tiled": _lib.KERNEL_TILED}
+            "tiled": _lib.KERNEL_TILED, "matrix": _lib.KERNEL_MATRIX}
 
 
 def distance_lut_cm(model: str = "moving_object") -> np.ndarray:
