@@ -58,8 +58,9 @@ struct MCfg {
     static constexpr int L_OFF = R_OFF + 16 * NRC;
     static constexpr int Z_OFF = L_OFF + 16 * NLC;       // one zero record
     static constexpr int X_OFF = Z_OFF + 16;             // exclusive prefix of V (256 i32)
-    static constexpr int T_OFF = X_OFF + 4 * 256;        // key table T(n) (NM i32)
-    static constexpr int LUT_OFF = T_OFF + 4 * 256;      // distance table (256 f64)
+    static constexpr int T_OFF = X_OFF + 4 * 256;        // key tables -T(n), two rows (2 x 256 i32)
+    static constexpr int M_OFF = T_OFF + 8 * 256;        // window byte masks by first ring slot (16 x 16 B)
+    static constexpr int LUT_OFF = M_OFF + 16 * 16;      // distance table (256 f64)
     static constexpr int SMEM = LUT_OFF + 8 * 256;
     static_assert(WIN <= 11, "|SB - 2C| * 256 fits an i32 key for w <= 11");
     static_assert(NM <= 256, "key low byte: 255 - n");
@@ -75,8 +76,14 @@ __host__ __device__ constexpr uint64_t row_gt_col_mask(int r) {
     return m;
 }
 
+#ifndef USV_SSD_MFMA_ORDER
+#define USV_SSD_MFMA_ORDER 0  // 1: all MFMA chains of a block before its epilogues (more VGPRs)
+#endif
+#ifndef USV_SSD_MFMA_OCC
+#define USV_SSD_MFMA_OCC 3  // waves per SIMD the kernel is compiled for
+#endif
 template <int RAD, int DB>
-__global__ __launch_bounds__(64) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
+__global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
                                                       uint8_t* __restrict__ disp, double* __restrict__ dist,
                                                       MatchArgs a, int n_xt, int bands) {
     using C = MCfg<RAD, DB>;
@@ -102,84 +109,118 @@ __global__ __launch_bounds__(64) void ssd_mfma_kernel(const uint8_t* __restrict_
     const __amdgpu_buffer_rsrc_t rsrcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(R), (short)0, 0x7FFFFFFF, 0x00020000);
 
-    // every record starts empty (zero); the zero record; the distance table
+    // every record starts empty (zero); the zero record; the window masks; the distance table
     for (int i = l; i < (C::X_OFF) / 16; i += 64) reinterpret_cast<mi32x4*>(smem)[i] = mi32x4{0, 0, 0, 0};
+    if (l < 64) {  // mask f: bytes of ring slots f .. f + w - 1 (mod 16)
+        const int f = l >> 2, q = l & 3;
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (((4 * q + e - f) & 15) < WIN) m |= 0xFFu << (8 * e);
+        reinterpret_cast<uint32_t*>(smem + C::M_OFF)[l] = m;
+    }
     if (dist)
         for (int i = l; i < 256; i += 64) reinterpret_cast<double*>(smem + C::LUT_OFF)[i] = a.lut[i];
 
-    // row rho's staged bytes, lane l: R columns rs + l + 64 q (q < 4; records l + 64 q) and L columns
-    // ls + l + 64 q (q < 2), clamped to the image (replicate border).  Strided records keep the byte stores of
-    // one instruction on 8 banks per 32 lanes (4-way) where records 4l .. 4l+3 per lane would put them on 2.
-    auto load_row = [&](int rho, uint32_t (&vr)[4], uint32_t (&vl)[2]) {
-        const int y = min(max(rho, 0), a.H - 1);
-        const uint32_t base = (uint32_t)(y * a.pitch);
-        const int Wm1 = a.W - 1;
+    // a row's staged bytes, lane l: R columns rs + l + 64 q (q < 4; records l + 64 q), L columns ls + l + 64 q
+    // (q < 2), clamped to the image (replicate border).  Strided records keep the byte stores of one instruction
+    // on 8 banks per 32 lanes (4-way) where records 4l .. 4l+3 per lane would put them on 2.
+    const int Wm1 = a.W - 1;
+    auto row_base = [&](int rho) { return (uint32_t)(min(max(rho, 0), a.H - 1) * a.pitch); };
+    auto load_r = [&](int rho, uint32_t (&v)[4]) {
+        const uint32_t base = row_base(rho);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            vr[q] = l + 64 * q < C::NM + 16
-                        ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcR, base + (uint32_t)min(max(rs + l + 64 * q, 0), Wm1), 0, 0)
-                        : 0x80u;
+            v[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcR, base + (uint32_t)min(max(rs + l + 64 * q, 0), Wm1), 0, 0);
+    };
+    auto load_l = [&](int rho, uint32_t (&v)[2]) {
+        const uint32_t base = row_base(rho);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            vl[q] = l + 64 * q < XT + 16
-                        ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcL, base + (uint32_t)min(max(ls + l + 64 * q, 0), Wm1), 0, 0)
-                        : 0x80u;
+            v[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrcL, base + (uint32_t)min(max(ls + l + 64 * q, 0), Wm1), 0, 0);
     };
-    // row rho's bytes (XOR 0x80: signed) into ring slot rho & 15 of the lane's records; 0x80 clears the slot of a
-    // row that left the window
-    auto put_row = [&](int rho, const uint32_t (&vr)[4], const uint32_t (&vl)[2]) {
-        const int slot = rho & 15;
+    // a row's bytes (XOR 0x80: signed) into ring slot rho & 15 of the lane's records.  The L records hold exactly
+    // the current window (0x80 clears the slot of a row that left): every B operand is then zero outside it.  The R
+    // records may run one row ahead (the next window's new row): A meets zero B bytes there, and SB masks slots.
+    auto put_r = [&](int rho, const uint32_t (&v)[4]) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) smem[C::R_OFF + 16 * (l + 64 * q) + slot] = (uint8_t)(vr[q] ^ 0x80u);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) smem[C::L_OFF + 16 * (l + 64 * q) + slot] = (uint8_t)(vl[q] ^ 0x80u);
+        for (int q = 0; q < 4; ++q) smem[C::R_OFF + 16 * (l + 64 * q) + (rho & 15)] = (uint8_t)(v[q] ^ 0x80u);
     };
-    const uint32_t kClearR[4] = {0x80u, 0x80u, 0x80u, 0x80u}, kClearL[2] = {0x80u, 0x80u};
+    auto put_l = [&](int rho, const uint32_t (&v)[2]) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) smem[C::L_OFF + 16 * (l + 64 * q) + (rho & 15)] = (uint8_t)(v[q] ^ 0x80u);
+    };
+    const uint32_t kClearL[2] = {0x80u, 0x80u};
+    // -T(n) of output row yy into table yy & 1: V(c) = Σ b'^2 over yy's window rows of R record c (masked dot4),
+    // X = its exclusive prefix (a DPP wave scan), SB(m) = X(n + w) - X(n)
+    auto make_table = [&](int yy) {
+        const mi32x4 mk = reinterpret_cast<const mi32x4*>(smem + C::M_OFF)[(yy - RAD) & 15];
+        const mi32x4* rec = reinterpret_cast<const mi32x4*>(smem + C::R_OFF);
+        int v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const mi32x4 rc = rec[4 * l + e];
+            int acc = 0;
+            acc = __builtin_amdgcn_sdot4(rc.x & mk.x, rc.x, acc, false);
+            acc = __builtin_amdgcn_sdot4(rc.y & mk.y, rc.y, acc, false);
+            acc = __builtin_amdgcn_sdot4(rc.z & mk.z, rc.z, acc, false);
+            acc = __builtin_amdgcn_sdot4(rc.w & mk.w, rc.w, acc, false);
+            v[e] = acc;
+        }
+        const int p1 = v[0] + v[1], p2 = p1 + v[2], tot = p2 + v[3];
+        // inclusive scan of the lane totals: row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31
+        int incl = tot;
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
+        const int ex = incl - tot;
+        reinterpret_cast<mi32x4*>(smem + C::X_OFF)[l] = mi32x4{ex, ex + v[0], ex + p1, ex + p2};
+        const int* X = reinterpret_cast<const int*>(smem + C::X_OFF);
+        int* T = reinterpret_cast<int*>(smem + C::T_OFF + 1024 * (yy & 1));
+        int xa[(C::NM + 63) / 64], xb[(C::NM + 63) / 64];
+#pragma unroll
+        for (int q = 0; q < (C::NM + 63) / 64; ++q)
+            if (l + 64 * q < C::NM) {
+                xa[q] = X[l + 64 * q];
+                xb[q] = X[l + 64 * q + WIN];
+            }
+#pragma unroll
+        for (int q = 0; q < (C::NM + 63) / 64; ++q)
+            if (l + 64 * q < C::NM) T[l + 64 * q] = l + 64 * q - 255 - ((xb[q] - xa[q]) << 8);  // -T(n)
+    };
 
-    // prologue: window rows y_begin - r .. y_begin + r - 1
-    for (int rho = y_begin - RAD; rho < y_begin + RAD; ++rho) {
-        uint32_t vr[4], vl[2];
-        load_row(rho, vr, vl);
-        put_row(rho, vr, vl);
+    // prologue: L rows y_begin - r .. y_begin + r - 1, R rows y_begin - r .. y_begin + r, the first row's table
+    for (int rho = y_begin - RAD; rho <= y_begin + RAD; ++rho) {
+        uint32_t vr[4];
+        load_r(rho, vr);
+        put_r(rho, vr);
+        if (rho < y_begin + RAD) {
+            uint32_t vl[2];
+            load_l(rho, vl);
+            put_l(rho, vl);
+        }
     }
-    uint32_t pr[4], pl[2];  // the next entering row's bytes, loaded one row ahead
-    load_row(y_begin + RAD, pr, pl);
+    make_table(y_begin);
+    uint32_t pr[4], pl[2];  // loaded one row ahead: R row y + 1 + r, L row y + r
+    load_r(y_begin + 1 + RAD, pr);
+    load_l(y_begin + RAD, pl);
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const mi32x4* recR = reinterpret_cast<const mi32x4*>(smem + C::R_OFF);
     const mi32x4* recL = reinterpret_cast<const mi32x4*>(smem + C::L_OFF);
 
     for (int y = y_begin; y < y_end; ++y) {
-        // the window's new row y + r enters, the row y - r - 1 left (its slot is cleared); fetch the next one
-        if (y > y_begin) put_row(y - RAD - 1, kClearR, kClearL);
-        put_row(y + RAD, pr, pl);
-        if (y + 1 < y_end) load_row(y + 1 + RAD, pr, pl);
-
-        // V(c) = Σ b'^2 over the window (R record c), X = its exclusive prefix, T(n) for the tile's NM centres
-        {
-            int v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const mi32x4 rc = recR[4 * l + e];
-                int s = 0;
-                s = __builtin_amdgcn_sdot4(rc.x, rc.x, s, false);
-                s = __builtin_amdgcn_sdot4(rc.y, rc.y, s, false);
-                s = __builtin_amdgcn_sdot4(rc.z, rc.z, s, false);
-                s = __builtin_amdgcn_sdot4(rc.w, rc.w, s, false);
-                v[e] = s;
-            }
-            const int p1 = v[0] + v[1], p2 = p1 + v[2], tot = p2 + v[3];
-            int incl = tot;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(incl, off, 64);
-                if (l >= off) incl += t;
-            }
-            const int ex = incl - tot;
-            reinterpret_cast<mi32x4*>(smem + C::X_OFF)[l] = mi32x4{ex, ex + v[0], ex + p1, ex + p2};
-            const int* X = reinterpret_cast<const int*>(smem + C::X_OFF);
-            int* T = reinterpret_cast<int*>(smem + C::T_OFF);
-#pragma unroll
-            for (int n = l; n < C::NM; n += 64) T[n] = n - 255 - ((X[n + WIN] - X[n]) << 8);  // -T(n)
+        // L: row y + r enters the window, row y - r - 1 left; R: row y + 1 + r for the next row's table
+        if (y > y_begin) put_l(y - RAD - 1, kClearL);
+        put_l(y + RAD, pl);
+        const bool more = y + 1 < y_end;
+        if (more) {
+            put_r(y + 1 + RAD, pr);
+            load_r(y + 2 + RAD, pr);
+            load_l(y + 1 + RAD, pl);
+            make_table(y + 1);  // independent of this row's MFMAs: the compiler interleaves the two
         }
         // B operands (L records): sub-tile t, K-step s -> window column dx = 2 s + h of output column x0 + 32 t + j
         mi32x4 Bop[NS][NSTEP];
@@ -198,17 +239,30 @@ __global__ __launch_bounds__(64) void ssd_mfma_kernel(const uint8_t* __restrict_
             mi32x4 Aop[NSTEP];
 #pragma unroll
             for (int s = 0; s < NSTEP; ++s) Aop[s] = recR[32 * b + j + 2 * s + h];
-            const mi32x4* Tb = reinterpret_cast<const mi32x4*>(smem + C::T_OFF + 4 * (32 * b + 4 * h));
+            const mi32x4* Tb = reinterpret_cast<const mi32x4*>(smem + C::T_OFF + 1024 * (y & 1) + 4 * (32 * b + 4 * h));
             mi32x4 Tv[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) Tv[g] = Tb[2 * g];  // rows 8 g + 4 h .. + 3 of the block
-#pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                if (b < t || b > t + DB) continue;
+            // USV_SSD_MFMA_ORDER 1: both sub-tiles' MFMA chains first, then the epilogues (the matrix pipe runs
+            // sub-tile 1's chain while the VALU reduces sub-tile 0's block; two accumulators live)
+            mi32x16 accs[NS];
+            auto chain = [&](int t) {
                 mi32x16 acc = {};
 #pragma unroll
                 for (int s = 0; s < NSTEP; ++s)
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aop[s], Bop[t][s], acc, 0, 0, 0);
+                accs[t] = acc;
+            };
+            if constexpr (USV_SSD_MFMA_ORDER == 1) {
+#pragma unroll
+                for (int t = 0; t < NS; ++t)
+                    if (b >= t && b <= t + DB) chain(t);
+            }
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                if (b < t || b > t + DB) continue;
+                if constexpr (USV_SSD_MFMA_ORDER != 1) chain(t);
+                const mi32x16 acc = accs[t];
                 int k[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) k[r] = (acc[r] << 9) + Tv[r >> 2][r & 3];  // -key: one v_lshl_add_u32
@@ -241,7 +295,7 @@ hipError_t launch_mfma_rd(const MatchArgs& a, hipStream_t s) {
     using C = MCfg<RAD, DB>;
     const int n_xt = (a.W + C::XT - 1) / C::XT;
 #ifndef USV_SSD_MFMA_WAVES
-#define USV_SSD_MFMA_WAVES 8  // target resident waves per CU (one-wave workgroups)
+#define USV_SSD_MFMA_WAVES 12  // target resident waves per CU (one-wave workgroups)
 #endif
     const long target = (long)cu_count() * USV_SSD_MFMA_WAVES;
     long bands = (target + (long)n_xt * a.batch - 1) / ((long)n_xt * a.batch);
