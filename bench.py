@@ -7,6 +7,11 @@ f64) -- one "step" = one pair through the hot path with inputs resident in
 HBM.  N GPUs = weak scaling (config D at N=8): every rank owns one pair per
 step (independent, no data-path collective) and rank 0 gathers the u8
 disparity maps over RCCL (xGMI), overlapped with the next step's compute.
+Consecutive steps are independent frames and alternate over two HIP streams
+(--streams, default 2), so the tail of frame k's launch -- its last
+workgroups, when most CUs are already idle -- overlaps the head of frame
+k+1's, as a frame server keeps two frames in flight; ms_per_step is then
+below the isolated launch time kernel_ms, which stays the roofline basis.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
@@ -65,6 +70,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="CPU-baseline sample budget: warm-up + 5 timed runs share it (N=1 only)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--streams", type=int, default=2,
+                   help="HIP streams the timed steps alternate over (consecutive frames are independent, so "
+                        "with 2 one launch's tail overlaps the next launch's head)")
     p.add_argument("--no-parity", action="store_true",
                    help="skip the oracle parity checks after the timed region (profiling passes only)")
     p.add_argument("--extra-steps", type=int, default=20,
@@ -816,7 +824,7 @@ def main():
     Lt = torch.from_numpy(L).to(dev)[i0:i1]
     Rt = torch.from_numpy(R).to(dev)[i0:i1]
     matcher = StereoBlockMatcher(D, w)
-    nbuf = 2
+    nbuf = max(2, a.streams)
     # (bands: one spare row so every rank can send band_w rows from y0 - i0 without a copy)
     disp_bufs = [torch.empty((1, rows + (1 if bands else 0), W), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     dist_bufs = [torch.empty((rows, W), dtype=torch.float64, device=dev) for _ in range(nbuf)] if with_dist else None
@@ -825,22 +833,23 @@ def main():
         shape = (band_w, W) if bands else (1, H, W)
         recv = [[torch.empty(shape, dtype=torch.uint8, device=dev) for _ in range(world)] for _ in range(nbuf)]
     stream = torch.cuda.current_stream()
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.streams) - 1)]
     pending = [None] * nbuf
     # one pre-marshalled C-ABI launcher per output buffer (StereoBlockMatcher.bind): a step enqueues its
     # match with one ctypes call, the same usv_sad_disparity_ex entry point compute() uses
     launch = [matcher.bind(Lt, Rt, out_disp=disp_bufs[b][0, :rows], out_dist=dist_bufs[b] if with_dist else None,
-                           stream=stream) for b in range(nbuf)]
+                           stream=streams[b % len(streams)]) for b in range(nbuf)]
 
-    def step(i, ev_pair=None):
+    def step(i):
         b = i % nbuf
         if pending[b] is not None:  # the gather that last read this buffer must finish first
             pending[b].wait()
             pending[b] = None
-        if ev_pair is not None:
-            ev_pair[0].record(stream)
         launch[b]()
-        if ev_pair is not None:
-            ev_pair[1].record(stream)
+        with torch.cuda.stream(streams[b % len(streams)]):  # the gather is ordered behind this frame only
+            collect(b)
+
+    def collect(b):
         if bands and a.gather != "none":
             # rank 0 collects the bands (band_w rows from each; a rank's extra row is ignored)
             work = dist.gather(disp_bufs[b][0, y0 - i0:y0 - i0 + band_w], recv[b] if rank == 0 else None,
@@ -907,9 +916,13 @@ def main():
     # back-to-back pass after it (kernel_ms).
     span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    # (the device was synchronised above: the side streams are idle, nothing to order them behind)
     span[0].record(stream)
     for i in range(a.steps):
         step(i)
+    t_enq = time.perf_counter()
+    for extra in streams[1:]:
+        stream.wait_stream(extra)
     span[1].record(stream)
     for b in range(nbuf):
         if pending[b] is not None:
@@ -919,6 +932,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    enqueue_us = (t_enq - t0) / a.steps * 1e6
     span_ms = span[0].elapsed_time(span[1]) / a.steps
     if a.kernel_steps > 0:
         kern_ms = time_launches(launch[0], a.kernel_steps, stream, preload="self") / 1e3
@@ -983,6 +997,11 @@ def main():
                           "enqueue time is hidden) after 10 ms of warm launches, kernel's stream"
                           if a.kernel_steps > 0 else "HIP events around the timed region, span / steps"),
         "span_ms_per_step": span_ms,
+        "host_enqueue_us_per_step": enqueue_us,
+        "streams": len(streams),
+        "stream_note": ("consecutive steps (independent frames) alternate over %d HIP streams, so a launch's "
+                        "tail overlaps the next launch's head; kernel_ms is one launch alone" % len(streams)
+                        if len(streams) > 1 else "one stream: launches strictly back to back"),
         "roofline": {
             "bound": "hbm",
             "achieved": achieved_gbs,

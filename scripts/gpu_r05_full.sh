@@ -16,5 +16,6 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [ -z "$NO_TESTS" ] && step pytest 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
 cp $OUT/bench.log $OUT/bench.json
+[ -n "$BENCH2" ] && step bench2 300 python bench.py --gpus 1 --steps 20 --warmup 5 && step bench_default 300 python bench.py
 [ -z "$NO_TRACE" ] && step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
 exit 0

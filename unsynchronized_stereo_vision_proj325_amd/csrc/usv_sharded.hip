@@ -117,11 +117,11 @@ usv_status complete(usv_sharded_engine* e, int si);
 
 // Complete slot si's batch because its slot is needed again; its status is kept for the wait on its
 // ticket (so a caller can tell a delivered batch from a failed one) instead of being reported by the
-// call that needed the slot.  The record holds the last 64 such batches.
+// call that needed the slot.  The record is unbounded (16 bytes per batch not waited for yet): dropping
+// entries would turn a failed implicit completion into "never submitted"; a wait erases its entry.
 void complete_implicit(usv_sharded_engine* e, int si) {
     const long long t = e->slot[si].ticket;
     const usv_status st = complete(e, si);
-    if (e->retired.size() >= 64) e->retired.erase(e->retired.begin());
     e->retired.push_back({t, st});
 }
 

@@ -295,11 +295,14 @@ hipError_t launch_mfma_rd(const MatchArgs& a, hipStream_t s) {
     using C = MCfg<RAD, DB>;
     const int n_xt = (a.W + C::XT - 1) / C::XT;
 #ifndef USV_SSD_MFMA_WAVES
-#define USV_SSD_MFMA_WAVES 12  // target resident waves per CU (one-wave workgroups)
+#define USV_SSD_MFMA_WAVES 32  // workgroups per CU the grid aims for (one-wave workgroups)
+#endif
+#ifndef USV_SSD_MFMA_MINROWS
+#define USV_SSD_MFMA_MINROWS 8  // shortest band (output rows per workgroup)
 #endif
     const long target = (long)cu_count() * USV_SSD_MFMA_WAVES;
     long bands = (target + (long)n_xt * a.batch - 1) / ((long)n_xt * a.batch);
-    bands = std::max(1L, std::min(bands, (long)std::max(1, a.H / 4)));
+    bands = std::max(1L, std::min(bands, (long)std::max(1, a.H / USV_SSD_MFMA_MINROWS)));
     const long total = (long)n_xt * bands * a.batch;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((ssd_mfma_kernel<RAD, DB>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a,
