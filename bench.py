@@ -423,7 +423,7 @@ def e2e_leg(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> di
 
     H, W = L.shape
     out = {}
-    for depth in (2, 3, 4):
+    for depth in (2, 3):  # (depth 4 measured slower than 3 in rounds 3-5: DESIGN.md section 7)
         fs = FrameStream(W, H, D, w, depth=depth)
         # frames already in each slot's pinned staging (a camera driver would DMA them there)
         staged = []
@@ -570,59 +570,82 @@ def frame_chain_fused_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> di
                       "map" % (w, D), "launches_per_frame": 3, "matches_six_launch_chain": same}
 
 
-def frame_chain_graph_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
-    """The same per-frame chain replayed as one HIP graph: the two cameras' frame prep forked onto a
-    second stream inside the graph (they are independent until the matcher), two frames per graph so
-    the frame-prep workspaces alternate their histogram parity as in eager use.  Checked against the
-    eager chain on the same input (disparity and distance maps bit-identical)."""
-    from unsynchronized_stereo_vision_proj325_amd.preproc import FramePrep
-    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, rectify_pair, synthetic_calibration
+def time_alternating(fns, streams, steps: int, warm_ms: float = 10.0) -> float:
+    """Average period (us) of `steps` calls that alternate over (fn, stream) pairs -- frame i runs fns[i % n]
+    on streams[i % n] -- after `warm_ms` of warm calls and `steps` untimed calls preloaded ahead of the
+    timed ones (as time_launches(preload="self")); HIP events on streams[0], joined with the others at
+    the end."""
+    n = len(fns)
+
+    def run(k):
+        for i in range(k):
+            with torch.cuda.stream(streams[i % n]):
+                fns[i % n]()
+
+    run(2 * n)
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
+    while (time.perf_counter() - t_w) * 1e3 < warm_ms:
+        run(4 * n)
+        torch.cuda.synchronize()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    run(steps)
+    start.record(streams[0])
+    run(steps)
+    for s in streams[1:]:
+        streams[0].wait_stream(s)
+    end.record(streams[0])
+    end.synchronize()
+    return start.elapsed_time(end) / steps * 1e3
+
+
+def frame_chain_overlap_leg(dev, W: int, H: int, D: int, w: int, steps: int) -> dict:
+    """The fused three-launch chain (frame_chain_fused_leg) with consecutive frames alternating over two
+    HIP streams, each with its own workspaces and outputs: frame k+1's memory-bound rectify / prep stage
+    shares the chip with frame k's VALU-bound matcher, as a camera pipeline keeps two frames in flight.
+    Each stream's maps are checked against the one-stream chain on the same input.  (This replaces the
+    round-4 hipGraph form of the six-launch chain: replaying it was slower than eager, 112.9 vs 107.5 us,
+    because the graph adds per-node overhead while the chain's cost is the kernels themselves.)"""
+    from unsynchronized_stereo_vision_proj325_amd.preproc import FramePrepPair
+    from unsynchronized_stereo_vision_proj325_amd.rectify import Rectifier, synthetic_calibration
 
     rng = np.random.default_rng(11)
     cl, cr = synthetic_calibration(W, H, seed=2)
-    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)  # packed maps (4 B/px)
-    ul, ur = (Rectifier(*cl, (W, H), device=dev, packed=False),
-              Rectifier(*cr, (W, H), device=dev, packed=False))  # OpenCV's map pair (6 B/px)
-    mb = 4 if rl.pmap is not None else 6
+    rl, rr = Rectifier(*cl, (W, H), device=dev), Rectifier(*cr, (W, H), device=dev)
     src_l = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
     src_r = torch.from_numpy(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).to(dev)
-    rect_l, rect_r = torch.empty_like(src_l), torch.empty_like(src_r)
-    pl, pr = FramePrep(dev), FramePrep(dev)
-    bufs = [(torch.empty_like(src_l), torch.empty_like(src_l), torch.empty((H, W), dtype=torch.uint8, device=dev))
-            for _ in range(2)]
-    disp = torch.empty((H, W), dtype=torch.uint8, device=dev)
-    dist = torch.empty((H, W), dtype=torch.float64, device=dev)
     matcher = StereoBlockMatcher(D, w)
-    side = torch.cuda.Stream(dev)
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(device=dev)]
+    lanes = []
+    for _ in streams:
+        outs = [torch.empty_like(src_l) for _ in range(4)] + [torch.empty((H, W), dtype=torch.uint8, device=dev)
+                                                             for _ in range(2)]
+        lanes.append((FramePrepPair(dev), outs, torch.empty((H, W), dtype=torch.uint8, device=dev),
+                      torch.empty((H, W), dtype=torch.float64, device=dev)))
 
-    def frame():
-        main = torch.cuda.current_stream()
-        rectify_pair(rl, rr, src_l, src_r, rect_l, rect_r)
-        side.wait_stream(main)
-        pl(rect_l, *bufs[0])
-        with torch.cuda.stream(side):
-            pr(rect_r, *bufs[1])
-        main.wait_stream(side)
-        matcher.compute(bufs[0][2], bufs[1][2], with_distance=True, out_disp=disp, out_dist=dist)
+    def make(lane):
+        pair, outs, disp, dist = lane
 
-    for _ in range(4):  # eager warm-up (lazy tables, occupancy queries); even count keeps the parities aligned
-        frame()
+        def frame():
+            pair.rectify_prep(rl, rr, src_l, src_r, outs=outs)
+            matcher.compute(outs[4], outs[5], with_distance=True, out_disp=disp, out_dist=dist)
+        return frame
+
+    fns = [make(lane) for lane in lanes]
+    us = time_alternating(fns, streams, steps)
     torch.cuda.synchronize()
-    ref_disp, ref_dist = disp.clone(), dist.clone()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        frame()
-        frame()
-    disp.zero_()
-    g.replay()
+    pair, outs, disp, dist = lanes[0]
+    ref_pair = FramePrepPair(dev)
+    ref_outs = [torch.empty_like(o) for o in outs]
+    ref_pair.rectify_prep(rl, rr, src_l, src_r, outs=ref_outs)
+    ref_disp, ref_dist = matcher.compute(ref_outs[4], ref_outs[5], with_distance=True)
     torch.cuda.synchronize()
-    same = bool(torch.equal(disp, ref_disp) and torch.equal(dist.nan_to_num(), ref_dist.nan_to_num()))
-    reps = max(2, steps // 2)
-    us = time_launches(g.replay, reps, torch.cuda.current_stream(), graph_ok=False) / 2
-    return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s",
-            "stages": "one hipGraph per two frames: rectify pair -> frame prep L || frame prep R (two streams) "
-                      "-> SAD w=%d D=%d -> distance map" % (w, D),
-            "matches_eager": same}
+    same = all(bool(torch.equal(l[2], ref_disp) and torch.equal(l[3].nan_to_num(), ref_dist.nan_to_num()))
+               for l in lanes)
+    return {"us_per_frame": us, "value": W * H / (us * 1e-6), "unit": "disparity-pixels/s", "streams": 2,
+            "stages": "rectify + HSV + hist (pair) -> equalize/HSV2BGR/gray (pair) -> SAD w=%d D=%d -> distance "
+                      "map; frames alternate over two streams" % (w, D),
+            "matches_one_stream_chain": same}
 
 
 def matcher_leg(dev, n: int = 150, max_pts: int = 120, runs: int = 5) -> dict:
@@ -1035,8 +1058,8 @@ def main():
     if world == 1 and rank == 0 and a.extra_steps > 0:
         rec["e2e"] = e2e_leg(dev, L, R, D, w, a.extra_steps)
         rec["frame_chain"] = frame_chain_leg(dev, W, H, D, w, a.extra_steps)
-        rec["frame_chain_graph"] = frame_chain_graph_leg(dev, W, H, D, w, a.extra_steps)
         rec["frame_chain_fused"] = frame_chain_fused_leg(dev, W, H, D, w, a.extra_steps)
+        rec["frame_chain_overlap"] = frame_chain_overlap_leg(dev, W, H, D, w, a.extra_steps)
         rec["fallbacks"] = fallback_legs(dev, L, R, D, w, max(2, a.extra_steps // 4))
         rec["matcher"] = matcher_leg(dev)
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
