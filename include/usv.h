@@ -309,10 +309,13 @@ usv_status usv_contour_pair_scores(const double* desc_a, int n_a, const double* 
  * usv_generate_matching_list; same arguments, same output order and capacity rule, scores equal to
  * the host restatement's within the device log10 rounding).  The matcher object owns pinned staging,
  * device buffers for up to max_contours contours and max_points points per set, and a stream: one call
- * = one H2D copy, three launches (descriptors of each set; one wave per row of the score matrix keeps
- * v < 0.75 and compacts the row in j order with a ballot), one D2H copy, a host concatenation of the
- * rows in i order.  The current device at create time is the matcher's device; not thread-safe (one
- * object per caller thread).  Replaces the per-pair loop of P/Main.cpp:403-426.
+ * = one H2D copy, five launches (descriptors of each set; one wave per row of the score matrix keeps
+ * v < 0.75 and compacts the row in j order with a ballot; the row offsets; the rows gathered into one
+ * i-major list), one D2H of the list's length and head (the previous call's length, at least 256
+ * entries) and, only when the list is longer, one more D2H of the rest.  max_contours <= 16384; memory:
+ * max_contours^2 x 16 B pinned host and twice that on the device.  The current device at create time is
+ * the matcher's device; not thread-safe (one object per caller thread).  Replaces the per-pair loop of
+ * P/Main.cpp:403-426.
  */
 typedef struct usv_contour_matcher usv_contour_matcher;
 usv_status usv_contour_matcher_create(int max_contours, int max_points, usv_contour_matcher** out);

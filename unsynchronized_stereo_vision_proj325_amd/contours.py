@@ -116,6 +116,22 @@ class ContourMatcherGPU:
 
 _MATCHERS: dict[int, ContourMatcherGPU] = {}
 _MATCHERS_LOCK = __import__("threading").Lock()
+# The matcher holds max_contours^2 x 16 B of pinned host memory and twice that on the device (score rows and
+# the compacted list): the per-device cache keeps one of at most _CACHE_MAX_CONTOURS contours (4096: 268 MB
+# pinned); larger sets get a matcher for the call only, and sets above the C matcher's limit take the
+# descriptor + score launches with the selection done by torch on the device.
+_CACHE_MAX_CONTOURS = 4096
+_MATCHER_MAX_CONTOURS = 16384  # usv_contour_matcher_create's limit
+
+
+def _select_on_device(contours_l, contours_r, dev):
+    """contour_descriptors + contour_pair_scores, then v < 0.75 (NaN fails) kept in row-major order."""
+    scores = contour_pair_scores(contour_descriptors(contours_l, dev), contour_descriptors(contours_r, dev))
+    keep = scores < 0.75
+    ij = torch.nonzero(keep)  # row-major: i-major, j-minor as P/Main.cpp:408-420
+    vals = scores[keep]
+    ij, vals = ij.cpu().tolist(), vals.cpu().tolist()
+    return [(i, j, v) for (i, j), v in zip(ij, vals)]
 
 
 def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
@@ -130,9 +146,20 @@ def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     n = max(len(contours_l), len(contours_r))
     p = max(sum(len(c) for c in contours_l), sum(len(c) for c in contours_r))
+    if n > _MATCHER_MAX_CONTOURS:
+        with torch.cuda.device(idx):
+            return _select_on_device(contours_l, contours_r, torch.device("cuda", idx))
+    if n > _CACHE_MAX_CONTOURS:
+        with torch.cuda.device(idx):
+            m = ContourMatcherGPU(n, max(1 << 16, p))
+        try:
+            return m(contours_l, contours_r)
+        finally:
+            m.close()
     with _MATCHERS_LOCK:
         m = _MATCHERS.get(idx)
         if m is None or not m.fits(n, n, p, p):
+            # (a replaced matcher is freed when the last caller still using it drops it)
             with torch.cuda.device(idx):
                 m = ContourMatcherGPU(max(512, n), max(1 << 16, p))
             _MATCHERS[idx] = m

@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 
 #include "usv.h"
@@ -174,13 +175,51 @@ __global__ void __launch_bounds__(256) match_select_kernel(const double* __restr
     if (lane == 0) counts[i] = n;
 }
 
+// Exclusive prefix of the row counts (one block): offs[i] = matches before row i, offs[n] = the total.
+__global__ void __launch_bounds__(1024) match_offsets_kernel(const int* __restrict__ counts, int n,
+                                                             int* __restrict__ offs) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    int carry = 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + t;
+        int v = i < n ? counts[i] : 0;
+        part[t] = v;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+            const int add = t >= d ? part[t - d] : 0;
+            __syncthreads();
+            part[t] += add;
+            __syncthreads();
+        }
+        if (i < n) offs[i] = carry + part[t] - v;
+        carry += part[1023];
+        __syncthreads();
+    }
+    if (t == 0) offs[n] = carry;
+}
+
+// Row i's matches (rows n_b apart) to dense[offs[i] ..]: the whole list in i-major, j-minor order, so one
+// copy of `total` entries brings it to the host.  One wave per row.
+__global__ void __launch_bounds__(256) match_gather_kernel(const usv_match* __restrict__ rows, int n_a, int n_b,
+                                                           const int* __restrict__ counts,
+                                                           const int* __restrict__ offs,
+                                                           usv_match* __restrict__ dense) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n_a) return;
+    const int c = counts[i], o = offs[i];
+    for (int k = lane; k < c; k += 64) dense[(size_t)o + k] = rows[(size_t)i * n_b + k];
+}
+
 }  // namespace
 }  // namespace usv
 
 // Device matcher object: pinned host staging for the two contour sets and the results, device buffers
 // sized for max_contours per set and max_points per set, one stream.  One call = one H2D copy of both
-// sets, the descriptor launch (both sets), the select launch, one D2H of counts + padded rows, and a
-// host concatenation of the rows in order.
+// sets, the descriptor launches, the select launch, the row offsets and the gather into one dense list on
+// the device, then one D2H of the total and of the list's first `guess` entries (the previous call's
+// total, at least 256) and, only when the list is longer, a second D2H of the rest.
 struct usv_contour_matcher {
     int max_n = 0, max_pts = 0, device = 0;
     hipStream_t stream = nullptr;
@@ -189,9 +228,11 @@ struct usv_contour_matcher {
     int* d_in = nullptr;
     double* d_desc = nullptr;   // 2 max_n x kDesc
     usv_match* d_rows = nullptr;  // max_n x max_n
-    int* d_counts = nullptr;      // max_n (followed in the same allocation by nothing else)
-    usv_match* h_rows = nullptr;  // pinned copy of d_rows
-    int* h_counts = nullptr;      // pinned
+    int* d_counts = nullptr;      // max_n row counts, then max_n + 1 row offsets
+    usv_match* d_dense = nullptr; // max_n x max_n: the compacted list
+    usv_match* h_rows = nullptr;  // pinned: the list's head (and rest)
+    int* h_counts = nullptr;      // pinned: the total
+    long long last_total = 256;   // D2H guess for the next call
 };
 
 extern "C" {
@@ -230,9 +271,10 @@ usv_status usv_contour_matcher_create(int max_contours, int max_points, usv_cont
               hipMalloc(&m->d_in, n_in * sizeof(int)) == hipSuccess &&
               hipMalloc(&m->d_desc, 2 * (size_t)max_contours * usv::kDesc * sizeof(double)) == hipSuccess &&
               hipMalloc(&m->d_rows, rows * sizeof(usv_match)) == hipSuccess &&
-              hipMalloc(&m->d_counts, (size_t)max_contours * sizeof(int)) == hipSuccess &&
+              hipMalloc(&m->d_counts, (2 * (size_t)max_contours + 1) * sizeof(int)) == hipSuccess &&
+              hipMalloc(&m->d_dense, rows * sizeof(usv_match)) == hipSuccess &&
               hipHostMalloc(&m->h_rows, rows * sizeof(usv_match), hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc(&m->h_counts, (size_t)max_contours * sizeof(int), hipHostMallocDefault) == hipSuccess;
+              hipHostMalloc(&m->h_counts, sizeof(int), hipHostMallocDefault) == hipSuccess;
     if (!ok) {
         usv_contour_matcher_destroy(m);
         return USV_ERR_HIP;
@@ -252,6 +294,7 @@ usv_status usv_contour_matcher_destroy(usv_contour_matcher* m) {
     (void)hipFree(m->d_desc);
     (void)hipFree(m->d_rows);
     (void)hipFree(m->d_counts);
+    (void)hipFree(m->d_dense);
     (void)hipHostFree(m->h_rows);
     (void)hipHostFree(m->h_counts);
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -306,23 +349,29 @@ usv_status usv_generate_matching_list_gpu(usv_contour_matcher* m, const int* pts
                        desc_b);
     hipLaunchKernelGGL(usv::match_select_kernel, dim3((unsigned)((n_a + 3) / 4)), dim3(256), 0, s, desc_a, n_a, desc_b,
                        n_b, m->d_rows, m->d_counts);
+    int* d_offs = m->d_counts + m->max_n;
+    hipLaunchKernelGGL(usv::match_offsets_kernel, dim3(1), dim3(1024), 0, s, m->d_counts, n_a, d_offs);
+    hipLaunchKernelGGL(usv::match_gather_kernel, dim3((unsigned)((n_a + 3) / 4)), dim3(256), 0, s, m->d_rows, n_a,
+                       n_b, m->d_counts, d_offs, m->d_dense);
     if (hipGetLastError() != hipSuccess) return fail(USV_ERR_HIP);
-    // rows are n_b apart on the device: copy the n_a x n_b block (packed by construction) and the counts
-    if (hipMemcpyAsync(m->h_counts, m->d_counts, (size_t)n_a * sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(m->h_rows, m->d_rows, (size_t)n_a * n_b * sizeof(usv_match), hipMemcpyDeviceToHost, s) !=
+    const long long most = (long long)n_a * n_b;
+    const long long guess = std::min(most, std::max(256LL, m->last_total));
+    if (hipMemcpyAsync(m->h_counts, d_offs + n_a, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(m->h_rows, m->d_dense, (size_t)guess * sizeof(usv_match), hipMemcpyDeviceToHost, s) !=
             hipSuccess)
         return fail(USV_ERR_HIP);
     if (hipStreamSynchronize(s) != hipSuccess) return USV_ERR_HIP;
-    long long total = 0;
-    for (int i = 0; i < n_a; ++i) total += m->h_counts[i];
+    const long long total = m->h_counts[0];
+    m->last_total = total;
     if (total > cap) return USV_ERR_INVALID_ARG;  // as usv_generate_matching_list: out must hold every match
-    int at = 0;
-    for (int i = 0; i < n_a; ++i) {
-        const int c = m->h_counts[i];
-        if (c > 0) std::memcpy(out + at, m->h_rows + (size_t)i * n_b, (size_t)c * sizeof(usv_match));
-        at += c;
+    if (total > guess) {
+        if (hipMemcpyAsync(m->h_rows + guess, m->d_dense + guess, (size_t)(total - guess) * sizeof(usv_match),
+                           hipMemcpyDeviceToHost, s) != hipSuccess)
+            return fail(USV_ERR_HIP);
+        if (hipStreamSynchronize(s) != hipSuccess) return USV_ERR_HIP;
     }
-    *n_out = at;
+    if (total > 0) std::memcpy(out, m->h_rows, (size_t)total * sizeof(usv_match));
+    *n_out = (int)total;
     return USV_OK;
 }
 

@@ -21,7 +21,7 @@
     defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) ||                                    \
     defined(USV_PAIR_GEN_WEIGHTS_NW2) || defined(USV_PAIR_GEN_G_X4) || defined(USV_SSD_FAST) ||                  \
     defined(USV_SSD_GEN_WEIGHTS) || defined(USV_PAIR) || defined(USV_PAIR_SMALL) || defined(USV_GROUP) ||        \
-    defined(USV_GROUP_OCC) || defined(USV_GROUP_NWG) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
+    defined(USV_GROUP_OCC) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
     defined(USV_GROUP_WEIGHTS) || defined(USV_PREP_THREADS) || defined(USV_HSV_PK) || defined(USV_PREP_KU) ||    \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
     defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD) ||   \

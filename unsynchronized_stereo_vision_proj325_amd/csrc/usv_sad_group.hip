@@ -298,7 +298,7 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
                       (!dist || ((reinterpret_cast<uintptr_t>(dist + x0) | ((uintptr_t)a.dist_pitch * 8)) & 15u) == 0);
     auto flush = [&](int rows) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
-        int tid = lane;
+        int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const uint32_t* crow = comb + cb * KRB * KW;
         if (wide) {
@@ -418,40 +418,27 @@ struct GroupPlan {
 #ifndef USV_GROUP_OCC
 #define USV_GROUP_OCC 3  // waves per SIMD the group kernel is compiled for
 #endif
-// Waves per workgroup.  Each wave is an independent band (its own LDS region, no barrier); the
-// workgroup only batches the dispatch.  Work item lin of the work map (usv_tiles.hpp, XCD = lin & 7)
-// belongs to wave w of block b with lin = ((b >> 3) NWG + w) 8 + (b & 7): the block's XCD is b & 7, as
-// the map assumes, and blocks b = 0 .. 8 k - 1 cover items 0 .. 8 k NWG - 1 once each.
-#ifndef USV_GROUP_NWG
-#define USV_GROUP_NWG 1
-#endif
-constexpr int kGroupNWG = USV_GROUP_NWG;
 template <int RAD, int G>
-__global__ __launch_bounds__(64 * kGroupNWG, USV_GROUP_OCC) void sad_group_kernel(const uint8_t* __restrict__ L,
+__global__ __launch_bounds__(64, USV_GROUP_OCC) void sad_group_kernel(const uint8_t* __restrict__ L,
                                                                      const uint8_t* __restrict__ R,
                                                                      uint8_t* __restrict__ disp,
                                                                      double* __restrict__ dist, MatchArgs a,
-                                                                     GroupPlan P, const uint2* __restrict__ tiles,
-                                                                     unsigned total) {
+                                                                     GroupPlan P, const uint2* __restrict__ tiles) {
     using C = GCfg<RAD, G>;
-    __shared__ __attribute__((aligned(16))) uint32_t smem_all[kGroupNWG * C::SMEM_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t smem[C::SMEM_WORDS];
     const int lane = threadIdx.x & 63;
-    const unsigned wv = kGroupNWG == 1 ? 0u : (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t* smem = smem_all + wv * C::SMEM_WORDS;
-    const unsigned lin = kGroupNWG == 1 ? blockIdx.x : ((blockIdx.x >> 3) * kGroupNWG + wv) * 8u + (blockIdx.x & 7u);
-    if (lin >= total) return;
     // work map of sad_pair_kernel (usv_tiles.hpp): XCD k owns the k-th contiguous run of tiles (x-tile
     // fastest, then band, then pair); normally one scalar load from the launcher's table
     unsigned xtu, pair;
     int y_begin, y_end;
     if (tiles) {
-        const uint2 t = tiles[lin];
+        const uint2 t = tiles[blockIdx.x];
         xtu = t.x & 0xFFFFu;
         pair = t.x >> 16;
         y_begin = (int)(t.y & 0xFFFFu);
         y_end = (int)(t.y >> 16);
     } else {
-        const TileSpan sp = tile_span(lin, total, P.n_xt, P.m, P.extra, P.gen_g, P.weights, a.H);
+        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P.n_xt, P.m, P.extra, P.gen_g, P.weights, a.H);
         xtu = sp.xt;
         pair = sp.pair;
         y_begin = sp.y_begin;
@@ -472,10 +459,9 @@ template <int RAD, int G>
 int resident_group_blocks_per_cu() {
     static const int n = [] {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_group_kernel<RAD, G>, 64 * kGroupNWG, 0) !=
-                hipSuccess || v <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_group_kernel<RAD, G>, 64, 0) != hipSuccess || v <= 0)
             v = 1;
-        return v * kGroupNWG;  // resident waves (work items) per CU
+        return v;
     }();
     return n;
 }
@@ -521,11 +507,8 @@ hipError_t launch_group_rg(const MatchArgs& a, hipStream_t s) {
     if (P.gen_g < 1) P.gen_g = 1;
     P.weights = per_cu == 12 && total > 2L * 8 * P.gen_g ? USV_GROUP_WEIGHTS : 0x01010101u;
     const uint2* tiles = tile_table(2, RAD * 16 + G, a, P.n_xt, P.m, P.extra, P.gen_g, P.weights, (unsigned)total, s);
-    // blocks: a multiple of 8 covering every item (see sad_group_kernel); one item per block when NWG = 1
-    const unsigned nblk = kGroupNWG == 1 ? (unsigned)total
-                                         : (((unsigned)total + 8u * kGroupNWG - 1) / (8u * kGroupNWG)) * 8u;
-    hipLaunchKernelGGL((sad_group_kernel<RAD, G>), dim3(nblk), dim3(64 * kGroupNWG), 0, s, a.L, a.R, a.disp, a.dist,
-                       a, P, tiles, (unsigned)total);
+    hipLaunchKernelGGL((sad_group_kernel<RAD, G>), dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist,
+                       a, P, tiles);
     return hipGetLastError();
 }
 
