@@ -866,7 +866,8 @@ def main():
     def step(i):
         b = i % nbuf
         if pending[b] is not None:  # the gather that last read this buffer must finish first
-            pending[b].wait()
+            with torch.cuda.stream(streams[b % len(streams)]):  # (wait() orders the current stream)
+                pending[b].wait()
             pending[b] = None
         launch[b]()
         with torch.cuda.stream(streams[b % len(streams)]):  # the gather is ordered behind this frame only
