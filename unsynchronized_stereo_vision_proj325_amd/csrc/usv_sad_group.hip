@@ -495,7 +495,14 @@ hipError_t launch_group_rg(const MatchArgs& a, hipStream_t s) {
     const long NC = (long)P.n_xt * a.batch;
     long m = slots / NC;
     if (m < 1) m = 1;
-    const long min_rows = USV_GROUP_MIN_BAND_ROWS > 0 ? USV_GROUP_MIN_BAND_ROWS : USV_GROUP_MIN_BAND_WINS * WIN;
+    // One-window bands are the optimum while they still give every CU ~8 waves (config B: 10.6).  Below that
+    // the frame is too small to fill the chip with them (config A: 480 one-window bands = 1.9 waves per CU)
+    // and bands down to 2 rows run faster despite the extra warm-up rows each (interleaved A/Bs: A 4.54 ->
+    // 4.29 us and 4.57 -> 4.33 us; B with 2-row bands 9.27 -> 9.39 us, so B keeps one-window bands;
+    // profiles/probes_r05/ab_group_rows_*_r05.txt, ab_group_pipe_*_r05.txt).
+    const bool underfilled = NC * (long)std::max(1, a.H / (USV_GROUP_MIN_BAND_WINS * WIN)) < 8L * group_cu_count();
+    const long min_rows = USV_GROUP_MIN_BAND_ROWS > 0 ? USV_GROUP_MIN_BAND_ROWS
+                                                      : (underfilled ? 2 : USV_GROUP_MIN_BAND_WINS * WIN);
     const long m_max = a.H / min_rows > 0 ? a.H / min_rows : 1;
     if (m > m_max) m = m_max;
     P.m = (int)m;
