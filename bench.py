@@ -457,12 +457,18 @@ def e2e_leg(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int) -> di
         out[f"depth{depth}"] = {"ms_per_frame": dt * 1e3, "value": W * H / dt}
         fs.close()
     best = min(out, key=lambda k: out[k]["ms_per_frame"])
-    disp = np.zeros((H, W), np.uint8)
-    t0 = time.perf_counter()
-    reps = 5
-    for _ in range(reps):
-        expand_distance(disp, threads=16)
-    expand_ms = (time.perf_counter() - t0) / reps * 1e3
+    # a frame-rate consumer expands into the same host map every frame (persistent workers, pages already
+    # mapped): median of 20 after 3 warm calls
+    disp = np.random.default_rng(3).integers(0, D, (H, W), dtype=np.uint8)
+    host_map = np.empty((H, W), dtype=np.float64)
+    for _ in range(3):
+        expand_distance(disp, threads=16, out=host_map)
+    ts = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        expand_distance(disp, threads=16, out=host_map)
+        ts.append(time.perf_counter() - t0)
+    expand_ms = float(np.median(ts)) * 1e3
 
     matcher = StereoBlockMatcher(D, w)
     hl, hr = torch.from_numpy(L).pin_memory(), torch.from_numpy(R).pin_memory()
