@@ -243,71 +243,6 @@ __global__ __launch_bounds__(kPT) void v_hist_kernel(HistJob j0, HistJob j1, int
     }
 }
 
-// The V-histogram pass over a DENSE frame (pitch = 3 W, W % 4 == 0, 4-byte aligned): the frame is one flat run of
-// W H / 4 twelve-byte quads, so a thread needs no row / column arithmetic -- quad q = blk kPT kDenseQ + t + u kPT
-// (u < kDenseQ, coalesced per u), all its loads issued before the block's LDS set-up.  Four quads per thread: the
-// stand-alone probe of this form ran 3.68 us at 1080p against 4.38 at two (profiles/probes_r05/hist_probe_r05.txt).
-// In the product (rocprof, profiles/probes_r05/ab_frame_stage_r05.txt) one camera takes 3.84-4.08 us minimum,
-// 4.3-5.9 median, against 4.92-5.0 / 5.4-6.7 for v_hist_kernel; two cameras 5.3-5.6 / 6.3-7.1 against 7.0-7.1 /
-// 7.6-8.3.  The flat-range kernel above, with its per-quad row division and byte path, stays for pitched frames.
-constexpr int kDenseQ = 4;
-__global__ __launch_bounds__(kPT) void v_hist_dense_kernel(HistJob j0, HistJob j1, int quads, int parity,
-                                                           int blocks_per_job) {
-    constexpr int NWV = kPT / 64;
-    const int job = (int)blockIdx.x >= blocks_per_job ? 1 : 0;
-    const int blk = (int)blockIdx.x - job * blocks_per_job;
-    const HistJob& j = job ? j1 : j0;
-    uint32_t* __restrict__ work = j.work;
-    __shared__ uint32_t lh[NWV][256];
-    const int t = threadIdx.x, wv = t >> 6;
-    const __amdgpu_buffer_rsrc_t rs = px_rsrc(j.bgr);
-    px_v3u q[kDenseQ];
-    // (block-uniform trip count: the set-up barrier inside the first sweep is reached by every thread)
-    for (int bb = blk * kPT * kDenseQ, first = 1; bb < quads; bb += blocks_per_job * kPT * kDenseQ, first = 0) {
-        const int base = bb + t;
-#pragma unroll
-        for (int u = 0; u < kDenseQ; ++u) {
-            const int qi = base + u * kPT;
-            q[u] = qi < quads ? __builtin_amdgcn_raw_buffer_load_b96(rs, (uint32_t)(12 * qi), 0, 0) : px_v3u{0, 0, 0};
-        }
-        if (first) {
-            for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
-            if (blk == 0 && t < 256)
-                for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
-            __syncthreads();
-        }
-#pragma unroll
-        for (int u = 0; u < kDenseQ; ++u) {
-            if (base + u * kPT >= quads) break;
-            const uint32_t w0 = q[u].x, w1 = q[u].y, w2 = q[u].z;  // B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3
-            const uint32_t v0 = max(max(w0 & 0xFFu, (w0 >> 8) & 0xFFu), (w0 >> 16) & 0xFFu);
-            const uint32_t v1 = max(max(w0 >> 24, w1 & 0xFFu), (w1 >> 8) & 0xFFu);
-            const uint32_t v2 = max(max((w1 >> 16) & 0xFFu, w1 >> 24), w2 & 0xFFu);
-            const uint32_t v3 = max(max((w2 >> 8) & 0xFFu, (w2 >> 16) & 0xFFu), w2 >> 24);
-            atomicAdd(&lh[wv][v0], 1u);
-            atomicAdd(&lh[wv][v1], 1u);
-            atomicAdd(&lh[wv][v2], 1u);
-            atomicAdd(&lh[wv][v3], 1u);
-        }
-    }
-    if (blk * kPT * kDenseQ >= quads) {  // a block with no quads still clears and contributes nothing
-        for (int i = t; i < NWV * 256; i += kPT) (&lh[0][0])[i] = 0;
-        if (blk == 0 && t < 256)
-            for (int c = 0; c < kHistCopies; ++c) work[kWHist + kParityWords * (1 - parity) + 256 * c + t] = 0;
-    }
-    __syncthreads();
-    if (t < 256) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) sum += lh[w][t];
-        if (sum) atomicAdd(&work[kWHist + kParityWords * parity + 256 * (blk % kHistCopies) + t], sum);
-    }
-}
-int dense_hist_blocks(int W, int H) {
-    const long long q = (long long)W * H / 4, per = (long long)kPT * kDenseQ;
-    return (int)std::min<long long>(4096, std::max<long long>(1, (q + per - 1) / per));
-}
-
 // One camera's equalize pass: the histogram it reads and the images it rewrites.
 struct EqJob {
     const uint32_t* work;
@@ -661,12 +596,7 @@ usv_status usv_frame_prep_u8(const uint8_t* bgr, int W, int H, int pitch, uint8_
     const usv::HistJob hj{bgr, pitch, nullptr, 0, static_cast<uint32_t*>(work)};
     const int nb = usv::prep_blocks(W, H), nbh = usv::prep_blocks(W, H, usv::kUHist);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (vh && pitch == 3 * W && W % 4 == 0) {
-        const int nbd = usv::dense_hist_blocks(W, H);
-        hipLaunchKernelGGL(usv::v_hist_dense_kernel, dim3(nbd), dim3(usv::kPT), 0, s, hj, hj, W * H / 4, parity, nbd);
-    } else {
-        hipLaunchKernelGGL(usv::v_hist_kernel, dim3(nbh), dim3(usv::kPT), 0, s, hj, hj, W, H, parity, nbh, vh);
-    }
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(nbh), dim3(usv::kPT), 0, s, hj, hj, W, H, parity, nbh, vh);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     const usv::EqJob ej{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch,
                         bgr, pitch};
@@ -691,16 +621,8 @@ usv_status usv_frame_prep_pair_u8(const uint8_t* bgrL, const uint8_t* bgrR, int 
                    usv::fits32(bgr_pitch, H);
     const int nb = usv::prep_blocks(W, H), nbh = usv::prep_blocks(W, H, usv::kUHist);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (vh && pitch == 3 * W && W % 4 == 0) {
-        const int nbd = usv::dense_hist_blocks(W, H);
-        hipLaunchKernelGGL(usv::v_hist_dense_kernel, dim3(2 * nbd), dim3(usv::kPT), 0, s,
-                           usv::HistJob{bgrL, pitch, nullptr, 0, wL}, usv::HistJob{bgrR, pitch, nullptr, 0, wR},
-                           W * H / 4, parity, nbd);
-    } else {
-        hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nbh), dim3(usv::kPT), 0, s,
-                           usv::HistJob{bgrL, pitch, nullptr, 0, wL}, usv::HistJob{bgrR, pitch, nullptr, 0, wR}, W, H,
-                           parity, nbh, vh);
-    }
+    hipLaunchKernelGGL(usv::v_hist_kernel, dim3(2 * nbh), dim3(usv::kPT), 0, s, usv::HistJob{bgrL, pitch, nullptr, 0, wL},
+                       usv::HistJob{bgrR, pitch, nullptr, 0, wR}, W, H, parity, nbh, vh);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
     hipLaunchKernelGGL(usv::equalize_kernel<true>, dim3(2 * nb), dim3(usv::kPT), 0, s,
                        usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch, bgrL, pitch},
