@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "usv.h"
+#include "usv_host_pool.hpp"
 #include "usv_kernels.hpp"
 
 namespace {
@@ -66,6 +67,9 @@ struct usv_sharded_engine {
         usv_status status;
     };
     std::vector<Retired> retired;
+    // workers for the per-GPU input copies of host batches (n > 1), started on the first such batch and joined
+    // by usv_sharded_destroy (usv_host_pool.hpp: per-call threads cost ~25-30 us each)
+    usv::HostPool pool;
 };
 
 namespace {
@@ -135,7 +139,8 @@ usv_status submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int
     const size_t shard_bytes = (size_t)e->per * frame;
 
     // 1. per GPU: inputs in (host batch -> its shard, or already resident), then one batched launch.
-    //    One host thread per GPU so the pageable-host H2D copies of different GPUs overlap.
+    //    Host batches: one persistent worker per GPU, so the pageable-host H2D copies of different GPUs overlap;
+    //    resident inputs: launches only, issued in turn from this thread (no copy to overlap).
     std::vector<usv_status> st(e->n, USV_OK);
     auto work = [&](int k) {
         int first = 0, count = 0;
@@ -165,12 +170,10 @@ usv_status submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int
         // call returns: wait for the copies (not the kernel) so the caller may reuse L / R at once.
         if (host_in && hipEventSynchronize(s.h2d[k]) != hipSuccess && st[k] == USV_OK) st[k] = USV_ERR_HIP;
     };
-    if (e->n == 1) {
-        work(0);
+    if (e->n == 1 || !host_in) {
+        for (int k = 0; k < e->n; ++k) work(k);
     } else {
-        std::vector<std::thread> th;
-        for (int k = 0; k < e->n; ++k) th.emplace_back(work, k);
-        for (auto& t : th) t.join();
+        e->pool.run(e->n, work);
     }
     for (usv_status x : st)
         if (x != USV_OK) {

@@ -18,14 +18,12 @@
 // for it (usv_distance_expand_host), so the link carries 1 B per pixel instead
 // of 9.  USV_STREAM_DEVICE_DIST keeps the f64 map on the device path as well.
 #include <algorithm>
-#include <condition_variable>
 #include <cstring>
 #include <functional>
-#include <mutex>
-#include <thread>
 #include <vector>
 
 #include "usv.h"
+#include "usv_host_pool.hpp"
 #include "usv_kernels.hpp"
 
 struct usv_frame_stream {
@@ -48,61 +46,9 @@ struct usv_frame_stream {
 
 namespace {
 
-// Persistent host workers for usv_distance_expand_host.  A frame-rate consumer calls it once per frame, and
-// starting its threads per call cost more than the expansion: 0.22 / 0.30 / 0.54 ms per 1080p map with 4 / 8 / 16
-// threads created per call on the GPU box (scripts/probes/expand_probe.py).  run(n, fn) executes fn(0 .. n-1),
-// part 0 on the calling thread; calls are serialised; workers are created on first use, grown on demand and
-// never destroyed (detached).
-class HostPool {
-  public:
-    void run(int n, const std::function<void(int)>& fn) {
-        std::lock_guard<std::mutex> call(call_mu_);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            while ((int)workers_.size() < n - 1) {
-                const int id = (int)workers_.size();
-                workers_.emplace_back([this, id] { loop(id); });
-                workers_.back().detach();
-            }
-            fn_ = &fn;
-            parts_ = n;
-            pending_ = n - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        fn(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_ == 0; });
-        fn_ = nullptr;
-    }
-
-  private:
-    void loop(int id) {
-        unsigned long long seen = 0;
-        for (;;) {
-            const std::function<void(int)>* fn;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (id + 1 >= parts_) continue;  // not needed by this call
-                fn = fn_;
-            }
-            (*fn)(id + 1);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
-        }
-    }
-    std::mutex call_mu_, mu_;
-    std::condition_variable cv_, done_;
-    std::vector<std::thread> workers_;
-    const std::function<void(int)>* fn_ = nullptr;
-    int parts_ = 0, pending_ = 0;
-    unsigned long long gen_ = 0;
-};
-
-HostPool& host_pool() {
-    static HostPool* pool = new HostPool;  // never destroyed: detached workers may outlive static destruction
+// the expansion's workers (usv_host_pool.hpp); never destroyed, so no worker is joined during static destruction
+usv::HostPool& host_pool() {
+    static usv::HostPool* pool = new usv::HostPool;
     return *pool;
 }
 
