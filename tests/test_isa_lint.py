@@ -310,6 +310,30 @@ def test_addtid_stores_see_one_dma_m0(fast_kernels):
     assert n_reuse > 0  # the reuse form is present in the build under test
 
 
+def test_addtid_reuse_offsets_address_the_transpose_buffer(fast_kernels):
+    # the reuse stores address tb as DMA M0 + offset, where the row DMA's M0 is
+    # rbase + 4 NRS ((I + PD) mod NB) and the store offset D0 = 4 TB_OFF - 4 NRS ((I + PD) mod NB).  So for every
+    # store group fed by a DMA's `s_add_u32 m0, <rbase>, <imm>` the sum imm + (first store's offset) is the same
+    # constant (4 TB_OFF) in the whole kernel: a reordered or added DMA between a row's DMA and its stores, or a
+    # slot / offset mismatch, breaks it.
+    checked = 0
+    for name, ins in fast_kernels.items():
+        reach = reaching_m0_writes(ins)
+        sums = set()
+        for k, i in enumerate(ins):
+            if not i.startswith("ds_write_addtid") or (k and ins[k - 1].startswith("ds_write_addtid")):
+                continue
+            (w,) = reach[k]
+            m = re.match(r"s_add_u32 m0, s\d+, (0x[0-9a-f]+|\d+)$", ins[w])
+            if not m:
+                continue
+            off = re.search(r"offset:(\d+)", i)
+            sums.add(int(m.group(1), 0) + (int(off.group(1)) if off else 0))
+            checked += 1
+        assert len(sums) <= 1, (name, sorted(sums))
+    assert checked > 0
+
+
 def test_lds_dma_m0_wait_state(fast_kernels):
     # GFX9: an SALU write of M0 needs one wait state before an LDS-DMA reads it
     for name, ins in fast_kernels.items():
