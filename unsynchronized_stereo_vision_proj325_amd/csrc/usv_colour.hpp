@@ -72,46 +72,5 @@ __device__ __forceinline__ void hsv2bgr_px(int H8, int S8, int V8, int& ob, int&
     orr = round_u8(r * 255.f);
 }
 
-// hsv2bgr_px for two pixels with the float arithmetic on packed f32 pairs (v_pk_mul_f32 /
-// v_pk_add_f32: the same IEEE operations in the same order, so the same bytes); the floor, the
-// sector selects and the conversions stay per pixel.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void hsv2bgr_px2(const int* H8, const int* S8, const int* V8, int* ob, int* og,
-                                            int* orr) {
-    f32x2 h = f32x2{(float)H8[0], (float)H8[1]} * (6.f / 180);
-    const f32x2 s = f32x2{(float)S8[0], (float)S8[1]} * (1.f / 255.f);
-    const f32x2 v = f32x2{(float)V8[0], (float)V8[1]} * (1.f / 255.f);
-    const f32x2 hw = h - 6.f;
-    h = f32x2{h.x >= 6 ? hw.x : h.x, h.y >= 6 ? hw.y : h.y};
-    const f32x2 fl = f32x2{floorf(h.x), floorf(h.y)};
-    int sec[2] = {(int)fl.x, (int)fl.y};
-    h = h - fl;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-        if ((unsigned)sec[i] >= 6u) {
-            sec[i] = 0;
-            h[i] = 0.f;
-        }
-    const f32x2 one = 1.f;
-    const f32x2 t0 = v, t1 = v * (one - s), t2 = v * (one - s * h), t3 = v * (one - s * (one - h));
-    f32x2 b, g, r;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int sector = sec[i];
-        b[i] = sector <= 1 ? t1[i] : sector == 2 ? t3[i] : sector <= 4 ? t0[i] : t2[i];
-        g[i] = sector == 0 ? t3[i] : sector <= 2 ? t0[i] : sector == 3 ? t2[i] : t1[i];
-        r[i] = sector == 0 ? t0[i] : sector == 1 ? t2[i] : sector <= 3 ? t1[i] : sector == 4 ? t3[i] : t0[i];
-    }
-    b = b * 255.f;
-    g = g * 255.f;
-    r = r * 255.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        ob[i] = round_u8(b[i]);
-        og[i] = round_u8(g[i]);
-        orr[i] = round_u8(r[i]);
-    }
-}
-
 }  // namespace
 }  // namespace usv

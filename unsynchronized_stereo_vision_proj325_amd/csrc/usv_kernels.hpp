@@ -12,21 +12,14 @@
 // included before any knob's default is defined, so a knob set on the command line of a product
 // build is an error here.
 #ifndef USV_VARIANT_BUILD
-#if defined(USV_STAMPS) || defined(USV_WGTIME) || defined(USV_PRIO) || defined(USV_SPLIT_CHAIN) ||              \
-    defined(USV_STATIC_RING) || defined(USV_RED_LDS) || defined(USV_RED_PACKED) || defined(USV_FAST_OCC) ||     \
-    defined(USV_L_WHOLE_WORD) || defined(USV_DMA_ONE_M0) || defined(USV_RUN_ADDR) || defined(USV_GEN_WEIGHTS) || \
-    defined(USV_ROUNDS) || defined(USV_MIN_BAND_WINS) || defined(USV_EXTRA_BANDS) || defined(USV_PAIR_PIPE) ||   \
-    defined(USV_NT_DIST) || defined(USV_WIDE_FLUSH) || defined(USV_PAIR_PIPE_R7) || defined(USV_PAIR_SPLIT_R) || \
-    defined(USV_PAIR_PREF) || defined(USV_PAIR_PIECE_OFF) || defined(USV_PAIR_OCC5) || defined(USV_PAIR_OCC7) || \
-    defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) ||                                    \
-    defined(USV_PAIR_GEN_WEIGHTS_NW2) || defined(USV_PAIR_GEN_G_X4) || defined(USV_SSD_FAST) ||                  \
-    defined(USV_SSD_GEN_WEIGHTS) || defined(USV_PAIR) || defined(USV_PAIR_SMALL) || defined(USV_GROUP) ||        \
-    defined(USV_GROUP_OCC) || defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_MIN_BAND_ROWS) ||            \
-    defined(USV_GROUP_WEIGHTS) || defined(USV_PREP_THREADS) || defined(USV_HSV_PK) || defined(USV_PREP_KU) ||    \
-    defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_REMAP_NT) || defined(USV_REMAP_BUF) ||     \
-    defined(USV_REMAP_LDS) || defined(USV_PAIR_STATIC) || defined(USV_PAIR_PD) || defined(USV_PAIR_LDS_PAD) ||   \
-    defined(USV_PAIR_RDASM) || defined(USV_PAIR_RDASM_GRP) || defined(USV_PAIR_ADDTID) || defined(USV_GROUP_LDSR) || \
-    defined(USV_SSD_LDSR) || defined(USV_PAIR_M0REUSE)
+#if defined(USV_GEN_WEIGHTS) || defined(USV_GROUP_LDSR) || defined(USV_GROUP_MIN_BAND_ROWS) ||                   \
+    defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_OCC) || defined(USV_GROUP_WEIGHTS) ||                  \
+    defined(USV_HIST_KU) || defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_NW2) ||                \
+    defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) || defined(USV_PAIR_M0REUSE) || defined(USV_PAIR_OCC5) ||              \
+    defined(USV_PAIR_OCC7) || defined(USV_PAIR_RDASM) || defined(USV_PREP_KU) || defined(USV_PREP_THREADS) ||    \
+    defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_SSD_GEN_WEIGHTS) ||                        \
+    defined(USV_SSD_LDSR) || defined(USV_SSD_MFMA_MINROWS) || defined(USV_SSD_MFMA_OCC) ||                       \
+    defined(USV_SSD_MFMA_WAVES) || defined(USV_STAMPS) || defined(USV_WGTIME)
 #error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
 #endif
 #define USV_BUILD_KIND "product build"

@@ -30,9 +30,6 @@ namespace {
 #ifndef USV_PREP_THREADS
 #define USV_PREP_THREADS 256  // threads per block of the two frame-prep kernels (512 / 1024 ran slower)
 #endif
-#ifndef USV_HSV_PK
-#define USV_HSV_PK 0  // 1: the equalize pass's HSV2BGR on packed f32 pairs (hsv2bgr_px2)
-#endif
 
 
 // Work buffer (include/usv.h USV_FRAME_PREP_WORK_BYTES): per parity (the
@@ -338,24 +335,6 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
                     in.c[3 * k + 2] = val;
                 }
             }
-#if USV_HSV_PK
-#pragma unroll
-            for (int k = 0; k < 4; ++k) in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
-#pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-                const int H2[2] = {in.c[3 * k], in.c[3 * k + 3]}, S2[2] = {in.c[3 * k + 1], in.c[3 * k + 4]},
-                          V2[2] = {in.c[3 * k + 2], in.c[3 * k + 5]};
-                int b[2], g[2], r[2];
-                hsv2bgr_px2(H2, S2, V2, b, g, r);
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    o.c[3 * (k + i)] = b[i];
-                    o.c[3 * (k + i) + 1] = g[i];
-                    o.c[3 * (k + i) + 2] = r[i];
-                    g4 |= (uint32_t)((b[i] * 1868 + g[i] * 9617 + r[i] * 4899 + (1 << 13)) >> 14) << (8 * (k + i));
-                }
-            }
-#else
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 in.c[3 * k + 2] = lut[in.c[3 * k + 2]];
@@ -366,7 +345,6 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
                 o.c[3 * k + 2] = r;
                 g4 |= (uint32_t)((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14) << (8 * k);
             }
-#endif
             store_px4(j.hsv, j.hsv_pitch, y, x, in, v, n);
             store_px4(j.bgr, j.bgr_pitch, y, x, o, v, n);
             uint8_t* go = j.gray + (size_t)y * j.gray_pitch + x;

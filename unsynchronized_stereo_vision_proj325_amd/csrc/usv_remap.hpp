@@ -8,12 +8,6 @@
 #include <cstddef>
 #include <cstdint>
 
-#ifndef USV_REMAP_NT
-#define USV_REMAP_NT 0
-#endif
-#ifndef USV_REMAP_BUF
-#define USV_REMAP_BUF 1  // source reads as raw-buffer loads: 32-bit offsets, no 64-bit address arithmetic
-#endif
 
 namespace usv {
 
@@ -154,17 +148,8 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
             my[k] = (int)(w4[k] >> 21) - 1;
         }
     } else if (vec_map && n == 4) {
-#if USV_REMAP_NT  // the maps are read once per frame: non-temporal loads
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        typedef unsigned v2u __attribute__((ext_vector_type(2)));
-        const v4i av = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(j.map1 + 2 * mrow));
-        const v2u fv = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(j.map2 + mrow));
-        const int4 a = make_int4(av[0], av[1], av[2], av[3]);
-        const uint2 f = make_uint2(fv[0], fv[1]);
-#else
         const int4 a = *reinterpret_cast<const int4*>(j.map1 + 2 * mrow);
         const uint2 f = *reinterpret_cast<const uint2*>(j.map2 + mrow);
-#endif
         const int w4[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -200,7 +185,6 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
         good |= in ? 1u << k : 0u;
         const uint32_t r0 = __umul24((uint32_t)yc, (uint32_t)j.spitch) + (uint32_t)ac;
         const uint32_t r1 = r0 + (uint32_t)(sH > 1 ? j.spitch : 0);
-#if USV_REMAP_BUF
         // a raw buffer over the source (stride 0, no range limit: the offsets stay inside the image): each
         // read is a 32-bit VGPR offset with the dword index in the instruction's immediate offset, instead
         // of a 64-bit address built per read
@@ -211,15 +195,6 @@ __device__ __forceinline__ void remap_quad(const RemapJob& j, int sW, int sH, in
             u0[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r0 + 4u * (uint32_t)i, 0, 0);
             u1[k][i] = __builtin_amdgcn_raw_buffer_load_b32(rs, r1 + 4u * (uint32_t)i, 0, 0);
         }
-#else
-        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(j.src + r0);
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(j.src + r1);
-#pragma unroll
-        for (int i = 0; i < NWD; ++i) {
-            u0[k][i] = q0[i];
-            u1[k][i] = q1[i];
-        }
-#endif
     }
     remap_blend<CN>(j, sW, sH, mx, my, mf, u0, u1, good, out);
 }

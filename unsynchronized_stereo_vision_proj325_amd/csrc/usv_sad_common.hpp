@@ -17,37 +17,10 @@ constexpr int kK = 16;  // outputs per x-tile
 #ifndef USV_STAMPS
 #define USV_STAMPS 0  // diagnostic build: per-phase s_memtime totals (scripts/stamps.py)
 #endif
-#ifndef USV_PRIO
-// Wave-priority rotation.  The SIMD arbitrates VALU issue by priority, then
-// age: with equal priorities the oldest of the three resident waves runs
-// nearly unimpeded and the youngest finishes ~27 us later on config C
-// (scripts/wgtime.py), so the launch ends in a one- and two-wave tail.
-// 1: rotate s_setprio by the wave's slot on its SIMD every flush; 2: by the
-// workgroup index (both waves of a workgroup share a phase); 3: by slot,
-// every input row; 0: off.
-#define USV_PRIO 0
-#endif
 #ifndef USV_WGTIME
 #define USV_WGTIME 0  // diagnostic build: per-workgroup start/end s_memrealtime + hardware id (scripts/wgtime.py)
 #endif
-#ifndef USV_SPLIT_CHAIN
-#define USV_SPLIT_CHAIN 0  // 1: two independent prefix chains per row (ILP); 0: one chain
-#endif
-#ifndef USV_STATIC_RING
-#define USV_STATIC_RING 0  // 1: WIN-slot R ring with compile-time slots (more LDS); 0: 8-slot dynamic ring
-#endif
-#ifndef USV_RED_LDS
-#define USV_RED_LDS 1  // argmin transpose through LDS (1) or permlane/DPP rounds (0)
-#endif
-#ifndef USV_RED_PACKED
-// 1: the LDS transpose stores the 8 packed (cost_x, cost_x+8) words instead of
-// 16 keys (half the ds_write), the reader builds the keys with v_perm from the
-// source lane's disparity (per-lane byte tables); 0: keys stored.
-#define USV_RED_PACKED 1
-#endif
-#ifndef USV_FAST_OCC
-#define USV_FAST_OCC 3  // target waves per SIMD (__launch_bounds__) for r <= 6: 3 -> <= 168 VGPRs
-#endif
+constexpr int kFastOcc = 3;  // target waves per SIMD (__launch_bounds__) of sad_fast_kernel for r <= 6: <= 168 VGPRs
 
 template <int RAD, int NW>
 struct Cfg {
@@ -61,22 +34,21 @@ struct Cfg {
     static constexpr int NR = NW * 63 + NPOS_V;  // R entries a wave reads per row
     static constexpr int NQ = (NR + 63) / 64;    // DMA instructions per R row
     static constexpr int NRS = NQ * 64;          // row-buffer stride (entries)
-    // Row buffers per wave.  With one or two waves the ring holds WIN rows, so
-    // in the row loop (unrolled WIN times) every buffer index, LDS offset and
-    // M0 value is a compile-time constant; four waves keep a 4-row ring.
-    static constexpr bool STATIC_RING = USV_STATIC_RING && NW <= 2;
-    static constexpr int NB = STATIC_RING ? WIN : (NW <= 2 ? 8 : 4);
+    // Row buffers per wave: an 8-row ring (slot t & 7), four waves a 4-row one.
+    static constexpr int NB = NW <= 2 ? 8 : 4;
     static constexpr int PD = NB - 1;            // rows in flight ahead of the one computed
     static constexpr int KRB = WIN;              // output rows per cross-wave combine
     static constexpr int LOFF = (4 - (RAD & 3)) & 3;  // (x0 - RAD) mod 4, x0 % 4 == 0
     // LDS carve (u32 words, every region 16-byte aligned)
     static constexpr int RBUF_OFF = 0;
-    // per-wave argmin transpose buffer: 16 pixels x 64 keys (USV_RED_LDS)
+    // per-wave argmin transpose buffer: 16 pixels x 64 keys (RED_LDS)
     static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
-    // (r = 6 with two waves sits at the 168-VGPR limit: the DPP rounds need fewer registers)
-    static constexpr bool RED_LDS = USV_RED_LDS && !(RAD == 6 && NW == 2);
-    // packed transpose (USV_RED_PACKED): +8 VGPRs of per-lane tables; r = 6 with one wave would spill
-    static constexpr bool RED_PACKED = USV_RED_PACKED && RED_LDS && !(RAD == 6 && NW == 1);
+    // argmin transpose through LDS (the other shape: permlane / DPP rounds); r = 6 with two waves sits at the
+    // 168-VGPR limit, where the DPP rounds need fewer registers
+    static constexpr bool RED_LDS = !(RAD == 6 && NW == 2);
+    // packed transpose: the 8 packed (cost_x, cost_x+8) words instead of 16 keys (half the ds_write), keys
+    // rebuilt by v_perm from per-lane d tables (+8 VGPRs; r = 6 with one wave would spill)
+    static constexpr bool RED_PACKED = RED_LDS && !(RAD == 6 && NW == 1);
     static constexpr int TB_WORDS = RED_LDS ? K * 64 : 0;
     static constexpr int COMB_OFF = TB_OFF + NW * TB_WORDS;
     static constexpr int LUT_OFF = COMB_OFF + 2 * KRB * NW * K;
@@ -124,11 +96,8 @@ struct LSeg {
 // overflow the packed u16 sums: interior tiles only (a window of w consecutive
 // positions holds at most ceil(w/4) such bytes), r <= 5: 11 rows x (11 x 255 +
 // 3 x 765) = 56 100 < 65 536.  Edge tiles replicate byte 0 and keep the mask.
-#ifndef USV_L_WHOLE_WORD
-#define USV_L_WHOLE_WORD 1
-#endif
 template <int RAD, int EDGE>
-constexpr bool kLWholeWord = USV_L_WHOLE_WORD && EDGE == 0 /* kInterior */ && RAD <= 5;
+constexpr bool kLWholeWord = EDGE == 0 /* kInterior */ && RAD <= 5;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -268,36 +237,22 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// LDS-DMA of one byte per lane (zero-extended to a dword at M0 + 4*lane),
-// saddr form: scalar row base + 32-bit lane offset.  GFX9 needs one wait
-// state between an SALU write of M0 and an LDS-DMA that reads it (the
-// compiler's hazard recognizer does not look inside inline asm): s_nop 0.  Inline asm so the
-// compiler cannot precompute 64-bit per-lane addresses for the look-ahead
-// rows (it hoisted and spilled them); the vmcnt waits are all explicit.
+// LDS address of a shared-memory pointer (the M0 / DS address operand of the inline-asm LDS ops below).
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
 }
-__device__ __forceinline__ void dma_u8(const uint8_t* row, uint32_t voff, uint32_t m0) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
-                 :: "v"(voff), "s"(row), "s"(m0) : "memory", "m0");
-}
-template <uint32_t OFF>
-__device__ __forceinline__ void dma_u8_at(const uint8_t* row, uint32_t voff, uint32_t lds_base) {
-    asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
-                 :: "v"(voff), "s"(row), "s"(lds_base), "n"(OFF) : "memory", "m0", "scc");
-}
 
-
-// A whole row's R DMAs under ONE M0 write: the immediate offset of an LDS-DMA
+// A whole row's R DMAs under ONE M0 write (LDS-DMA of one byte per lane, zero-extended to a dword at
+// M0 + 4 lane; inline asm so the compiler cannot precompute 64-bit per-lane addresses for the look-ahead rows --
+// it hoisted and spilled them -- and every vmcnt wait is explicit; GFX9 needs one wait state between an SALU
+// write of M0 and an LDS-DMA that reads it, which the compiler's hazard recognizer does not see inside asm:
+// s_nop 0).  The immediate offset of an LDS-DMA
 // moves the LDS destination and the global address alike
 // (scripts/probes/glds_offset_probe.hip), so DMA q uses offset:256 q and a
 // per-lane offset pre-biased by -256 q; the row pointer carries a -kDmaBias
 // bias so that every per-lane offset stays non-negative (the 32-bit VGPR
 // offset is zero-extended).  Saves the M0 write + wait state of every DMA but
 // the first.
-#ifndef USV_DMA_ONE_M0
-#define USV_DMA_ONE_M0 1
-#endif
 constexpr uint32_t kDmaBias = 1024;  // >= 256 (NQ - 1), NQ <= 5
 template <int NQ>
 __device__ __forceinline__ void dma_row(const uint8_t* rr_biased, const uint32_t (&vo)[NQ], uint32_t m0) {
@@ -330,18 +285,6 @@ __device__ __forceinline__ void dma_row(const uint8_t* rr_biased, const uint32_t
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() would also wait
 // vmcnt(0), draining the LDS-DMA look-ahead; the comb buffers are plain LDS
 // stores, so lgkmcnt(0) before the barrier is all the hand-off needs.
-__device__ __forceinline__ void set_prio(int p) {
-    if (p == 0) __builtin_amdgcn_s_setprio(0);
-    else if (p == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(2);
-}
-// The wave's slot on its SIMD (HW_ID.WAVE_ID), wave-uniform.
-__device__ __forceinline__ int wave_slot() {
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    return (int)(hw & 0xFu);
-}
-
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -420,9 +363,6 @@ __device__ __forceinline__ void unpack_words(const typename SWords<N>::T& w, uin
 // no range limit), the L row segment an s_load with an SGPR offset; both offsets are
 // running sums clamped at the last image row (two SALU per pointer and row instead of
 // clamp, multiply and a 64-bit add).  Warm-up rows keep the clamped per-row form.
-#ifndef USV_RUN_ADDR
-#define USV_RUN_ADDR 1
-#endif
 template <int NQ>
 __device__ __forceinline__ void dma_row_buf(su4 rsrc, uint32_t soff, const uint32_t (&vo)[NQ], uint32_t m0) {
     static_assert(NQ >= 1 && NQ <= 5, "1..5 DMAs per row");
@@ -565,20 +505,12 @@ int cu_count() {
     return n;
 }
 
-#ifndef USV_MIN_BAND_WINS
 // shortest band, in windows (w rows): the ring warm-up costs w rows per band.  Binds only on small frames
 // (1080p, D = 128 has 12-13 bands of ~85 rows); interleaved A/B at 640x480 w7 D64: 1 / 2 / 3 / 4 windows =
 // 29.5 / 22.2 / 20.5 / 22.5 us, at 320x240 w5 D32: 2 / 3 / 4 = 16.8 / 15.3 / 16.4 us
-// (profiles/probes/ab_minband_small_r01.txt, ab_weights_minband_r01.txt).
-#define USV_MIN_BAND_WINS 3
-#endif
-#ifndef USV_EXTRA_BANDS
-#define USV_EXTRA_BANDS 1  // one pair: give some x-tiles an extra band so the grid fills every resident slot
-#endif
-
-#ifndef USV_SSD_FAST
-#define USV_SSD_FAST 1  // 0: SSD always takes the tiled kernel
-#endif
+// (profiles/probes/ab_minband_small_r01.txt, ab_weights_minband_r01.txt).  With one pair some x-tiles take an
+// extra band so that the grid fills every resident slot.
+constexpr int kMinBandWins = 3;
 
 }  // namespace
 }  // namespace usv

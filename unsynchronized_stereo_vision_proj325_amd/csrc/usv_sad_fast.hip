@@ -109,7 +109,6 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     }
     const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const int s_l = NW * (63 - l_eff);  // this lane's first chain entry in a row buffer
-    const int prio_slot = USV_PRIO == 3 ? wave_slot() : 0;
     const int nout = y_end - y_begin;
     const int T = nout + 2 * RAD;  // input rows walked
     const int Hm1 = a.H - 1, Wm1 = a.W - 1;
@@ -122,8 +121,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         return (uint32_t)(y * a.pitch);
     };
     const uint8_t* const Lseg = L + LS::base(x0);
-    const uint8_t* const Rdma = (USV_DMA_ONE_M0 && !C::STATIC_RING) ? R - kDmaBias : R;
-    constexpr bool RUN = USV_RUN_ADDR && USV_DMA_ONE_M0 && !C::STATIC_RING;
+    const uint8_t* const Rdma = R - kDmaBias;  // (dma_row: one M0 per row, lane offsets biased by kDmaBias)
     // raw (unclamped) byte offsets of the rows the next steady row loads: L row t + 1, R row t + PD
     const int y0 = y_begin - RAD;
     const int last_off = Hm1 * a.pitch;
@@ -149,23 +147,10 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
     for (int i = 0; i < C::NQ; ++i) colRb[i] = colR[i] + kDmaBias - 256u * (uint32_t)i;
     const uint32_t rbase = lds_addr(rbuf);
-    // BUF >= 0: compile-time ring slot (static ring); BUF < 0: slot t & (NB-1)
-    auto issue_dma = [&](int t, auto buf_tag) {
-        constexpr int BUF = decltype(buf_tag)::value;
-        const uint8_t* rr = Rdma + row_off(t);
-        if constexpr (BUF >= 0) {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (dma_u8_at<4u * (BUF * C::NRS + 64 * Q)>(rr, colR[Q], rbase), ...);
-            }(std::make_integer_sequence<int, C::NQ>{});
-        } else if constexpr (USV_DMA_ONE_M0 && !C::STATIC_RING) {
-            const int buf = t & (NB - 1);
-            dma_row<C::NQ>(rr, colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
-        } else {
-            const int buf = t & (NB - 1);
-#pragma unroll
-            for (int i = 0; i < C::NQ; ++i)
-                dma_u8(rr, colR[i], rbase + 4u * (buf * C::NRS + 64 * i));
-        }
+    // row t into ring slot t & (NB - 1)
+    auto issue_dma = [&](int t) {
+        const int buf = t & (NB - 1);
+        dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
     };
 
     // ---- L bytes: the row segment through the scalar cache, one row ahead.
@@ -180,8 +165,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     st.t_begin = st.last = Stamps::now();
 #endif
     // One input row t = t0 + I (t0 a multiple of WIN): packed chain, H pairs,
-    // S / ring update.  I selects the ring slot (and, with the static ring,
-    // the row buffers) at compile time.
+    // S / ring update.  I selects the H ring slot at compile time.
     auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[HALF], uint32_t(&ring)[WIN][HALF]) {
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int I = decltype(i_tag)::value;
@@ -191,17 +175,14 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * NDMA>();  // row t has landed in LDS
         __builtin_amdgcn_wave_barrier();
-        if constexpr (USV_PRIO == 3) set_prio((prio_slot + t) % 3);
-        if constexpr (C::STATIC_RING) {
-            issue_dma(t + PD, std::integral_constant<int, (I + PD) % NB>{});
-        } else if constexpr (RUN && !WARM) {
+        if constexpr (!WARM) {
             int rr = rawR;
             asm volatile("" : "+s"(rr));  // opaque: one row's offset at a time
             const int buf = (t + PD) & (NB - 1);
             dma_row_buf<C::NQ>(rsrc, (uint32_t)min(rr, last_off), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
             rawR = rr + a.pitch;
         } else {
-            issue_dma(t + PD, std::integral_constant<int, -1>{});
+            issue_dma(t + PD);
         }
         USV_STAMP(0);
 
@@ -224,7 +205,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
         // Row-buffer offset as an opaque scalar: one v_add per row, instead
         // of the compiler keeping a VGPR base per static ring slot (the
         // ds_read2 offset field only spans 2 KB) live through the loop.
-        int boff = (C::STATIC_RING ? I % NB : (t & (NB - 1))) * C::NRS;
+        int boff = (t & (NB - 1)) * C::NRS;
         asm volatile("" : "+s"(boff));
         const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
         uint32_t Rv[C::NPOS_V];
@@ -238,25 +219,13 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #pragma unroll
             for (int e = 0; e < C::VEC; ++e) Rv[jv * C::VEC + e] = vget<C::VEC>(v, e);
         }
-        // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)]; with
-        // USV_SPLIT_CHAIN two independent chains: A covers steps [0, SP), B
-        // steps [SP, NSTEP) from zero, so P[j] = A[SP] + B[j - SP] for j > SP.
-        constexpr int SP = USV_SPLIT_CHAIN ? HALF : C::NSTEP;
-        constexpr int NB_STEPS = C::NSTEP - SP;
-        uint32_t A[SP + 1], Bc[NB_STEPS + 1];
+        // Packed prefix P[j] = [sum_{i<j} e(i), sum_{i<j} e(i + HALF)] (one chain: two independent
+        // half-chains for ILP measured no faster, round 1)
+        uint32_t A[C::NSTEP + 1];
         A[0] = 0;
-        Bc[0] = 0;
 #pragma unroll
-        for (int j = 0; j < (SP > NB_STEPS ? SP : NB_STEPS); ++j) {
-            if (j < SP)
-                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF],
-                                                      __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
-            if (j < NB_STEPS) {
-                const int jj = j + SP;
-                Bc[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[jj + HALF], Rv[jj + HALF],
-                                                       __builtin_amdgcn_sad_u8(Lv[jj], Rv[jj], Bc[j]));
-            }
-        }
+        for (int j = 0; j < C::NSTEP; ++j)
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j + HALF], Rv[j + HALF], __builtin_amdgcn_sad_u8(Lv[j], Rv[j], A[j]));
 #pragma unroll
         for (int x = 0; x < HALF; ++x) {
             // H pair (x, x + HALF) = P[x + WIN] - P[x].  Packed pairs, but
@@ -264,9 +233,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
             // monotone, S - ring is a w-1 row sum), so plain 32-bit add/sub
             // give the packed result exactly: v_add/v_sub_u32 issue at full
             // rate, v_pk_*_u16 at half rate (scripts/probes/valu_rate.hip).
-            uint32_t h;
-            if (x + WIN <= SP) h = A[x + WIN] - A[x];
-            else h = Bc[x + WIN - SP] + (A[SP] - A[x]);
+            const uint32_t h = A[x + WIN] - A[x];
             if constexpr (WARM) S[x] = S[x] + h;
             else S[x] = (S[x] - ring[I][x]) + h;
             ring[I][x] = h;
@@ -279,7 +246,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 #if USV_STAMPS
         st.rows++;
 #endif
-        if constexpr (RUN && !WARM) {
+        if constexpr (!WARM) {
             int rl = rawL;
             asm volatile("" : "+s"(rl));
             lw_next = s_load_words_off<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
@@ -296,10 +263,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
     // Output row o goes to combine slot o % KRB; with KRB = WIN the flush
     // points sit at fixed positions of the WIN-unrolled row loop.
     int cb = 0, y_chunk = y_begin;
-    int prio_phase = USV_PRIO == 2 ? (int)blockIdx.x : (USV_PRIO == 1 || USV_PRIO == 3 ? wave_slot() : 0);
-    if (USV_PRIO) set_prio(prio_phase % 3);
     auto flush = [&](int rows) {
-        if (USV_PRIO == 1 || USV_PRIO == 2) set_prio(++prio_phase % 3);
         lds_barrier();
         // opaque thread id: the flush's per-lane addresses must not be hoisted
         // out of the row loop (they would stay live through it and spill)
@@ -354,7 +318,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 
     // prologue: PD rows in flight, L words of row 0 requested
     [&]<int... P>(std::integer_sequence<int, P...>) {
-        (issue_dma(P, std::integral_constant<int, C::STATIC_RING ? P : -1>{}), ...);
+        (issue_dma(P), ...);
     }(std::make_integer_sequence<int, PD>{});
     load_lw(0);
 
@@ -405,7 +369,7 @@ __device__ __forceinline__ void band_loop(const uint8_t* __restrict__ L,
 
 // r = 7 (15-row ring) and r = 6 with four waves need more than 168 VGPRs:
 // two waves per SIMD instead of spilling (tests/test_isa_lint.py checks).
-constexpr int fast_occ(int rad, int nw) { return (rad >= 7 || (rad == 6 && nw == 4)) ? 2 : USV_FAST_OCC; }
+constexpr int fast_occ(int rad, int nw) { return (rad >= 7 || (rad == 6 && nw == 4)) ? 2 : kFastOcc; }
 
 template <int RAD, int NW>
 __global__ __launch_bounds__(NW * 64, fast_occ(RAD, NW)) void sad_fast_kernel(const uint8_t* __restrict__ L,
@@ -523,24 +487,21 @@ hipError_t launch_rn(const MatchArgs& a, hipStream_t s) {
     const int per_cu = resident_blocks_per_cu<RAD, NW>();
     const long slots = (long)cu_count() * per_cu;
     const long NC = (long)P.n_xt * a.batch;
-#ifndef USV_ROUNDS
-#define USV_ROUNDS 1  // workgroup rounds per launch (experiment: >1 = shorter bands, later rounds fill the tail)
-#endif
-    long m = slots * USV_ROUNDS / NC;
+    long m = slots / NC;
     if (m < 1) m = 1;
-    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    const long m_max = a.H / (kMinBandWins * WIN) > 0 ? a.H / (kMinBandWins * WIN) : 1;
     if (m > m_max) m = m_max;
     P.m = (int)m;
     // e.g. 1080p, D = 128: 1536 slots over 120 x-tiles = 12 bands + 96 x-tiles with a 13th
-    const long ex = slots * USV_ROUNDS - NC * m;
-    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && USV_ROUNDS == 1 && ex > 0 && ex < P.n_xt &&
-               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    const long ex = slots - NC * m;
+    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= kMinBandWins * WIN) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);
     if (P.gen_g < 1) P.gen_g = 1;
     // weighted only when every SIMD holds three waves of one round
-    const bool three = USV_ROUNDS == 1 && per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
+    const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
     P.weights = three ? USV_GEN_WEIGHTS : 0x01010101u;
     dim3 grid((unsigned)total), block(NW * 64);
     hipLaunchKernelGGL((sad_fast_kernel<RAD, NW>), grid, block, 0, s, a.L, a.R, a.disp, a.dist, a, P);
@@ -576,7 +537,7 @@ extern "C" __attribute__((visibility("default"))) int usv_debug_wgtime(unsigned 
 bool fast_path_supported(const MatchArgs& a) {
     // W % 4 == 0 and W >= 3 tiles: the border tiles' L maps are compile-time.  SSD (metric 1): the
     // SSD kernel's 8-column L segments exist for 11 <= w <= 15.
-    const bool metric_ok = a.metric == 0 || (USV_SSD_FAST && a.metric == 1 && a.w >= 11);
+    const bool metric_ok = a.metric == 0 || (a.metric == 1 && a.w >= 11);
     return metric_ok && a.w >= 3 && a.w <= 15 && (a.w & 1) && a.D >= 1 && a.D <= 256 &&
            (a.W % 4) == 0 && a.W >= 3 * kK && (a.pitch % 4) == 0 && (long long)a.pitch * a.H < (1LL << 31) &&
            (reinterpret_cast<uintptr_t>(a.L) % 4) == 0 &&

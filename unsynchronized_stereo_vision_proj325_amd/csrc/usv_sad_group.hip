@@ -531,12 +531,10 @@ hipError_t launch_group_g(const MatchArgs& a, hipStream_t s) {
 
 }  // namespace
 
-#ifndef USV_GROUP
-#define USV_GROUP 1  // the grouped paired kernel for even 16 < D <= 64 and 5 <= w <= 9
-#endif
+// the grouped paired kernel: even 16 < D <= 64, 5 <= w <= 9
 bool group_path_supported(const MatchArgs& a) {
     // (fast_path_supported holds: W % 4 == 0, W >= 48, 4-byte aligned bases and pitch, pitch * H < 2^31)
-    return USV_GROUP && a.metric == 0 && (a.D % 2) == 0 && a.D > 16 && a.D <= 64 && a.w >= 5 && a.w <= 9 &&
+    return a.metric == 0 && (a.D % 2) == 0 && a.D > 16 && a.D <= 64 && a.w >= 5 && a.w <= 9 &&
            a.W >= 32;
 }
 

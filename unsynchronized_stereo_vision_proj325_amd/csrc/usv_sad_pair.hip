@@ -25,9 +25,6 @@ namespace {
 // 8p + q the 8 packed words of pixel p from lanes 8q .. 8q + 7 (16 keys), then three DPP
 // rounds across the 8 lanes of the pixel.  Ties -> smallest d as before.
 // ===================================================================================
-#ifndef USV_WIDE_FLUSH
-#define USV_WIDE_FLUSH 1  // paired kernel: one 8-byte disparity store and one 16-byte distance store per lane per chunk
-#endif
 // Argmin transpose of row t finished during row t + 1 (latency hidden by the chain): r = 5 only (at
 // r = 6, 7 the held transpose words spill).
 template <int RAD>
@@ -50,38 +47,21 @@ struct PCfg {
 #ifndef USV_PAIR_RDASM
 #define USV_PAIR_RDASM 1  // staged-entry reads as single ds_read_b64 (inline asm, explicit lgkmcnt waits): C 51.70 -> 49.32 us
 #endif
-#ifndef USV_PAIR_RDASM_GRP
-#define USV_PAIR_RDASM_GRP 1  // staged-entry pairs retired per counted wait
-#endif
 #ifndef USV_PAIR_M0REUSE
 #define USV_PAIR_M0REUSE 1  // static ring: transpose stores off the row DMA's M0; row clamp in the DMA's wait state (SALU -2.9 per row)
 #endif
-#ifndef USV_PAIR_ADDTID
-#define USV_PAIR_ADDTID 1  // transpose stores as ds_write_addtid_b32 (C 52.33 -> 51.77 us, E 511.9 -> 508.0 us)
-#endif
-#ifndef USV_PAIR_STATIC
-#define USV_PAIR_STATIC 1
-#endif
-#ifndef USV_PAIR_PD
-#define USV_PAIR_PD 0  // rows of DMA look-ahead (0: NB - 1)
-#endif
-    static constexpr bool STATIC = USV_PAIR_STATIC && RAD == 5 && NW == 1;
+    // (transpose stores as ds_write_addtid_b32: C 52.33 -> 51.77 us, E 511.9 -> 508.0 us, round 4)
+    static constexpr bool STATIC = RAD == 5 && NW == 1;
     static constexpr int NB = STATIC ? WIN : 8;
-#ifndef USV_PAIR_SPLIT_R
-#define USV_PAIR_SPLIT_R 7  // radius from which the row's entries are read in two batches
-#endif
-    static constexpr int SPLIT = RAD >= USV_PAIR_SPLIT_R ? 2 : 1;
+    static constexpr int SPLIT = RAD >= 7 ? 2 : 1;  // r = 7 reads the row's entries in two batches
     // Chain jump: the row sums H[x] = A[x + WIN] - A[x] (x < K) read the prefix A only at 0..K-1 and
     // WIN..WIN+K-1, so the WIN - K + 1 increments j = K-1 .. WIN-1 between them are folded into quads:
     // one 4-byte v_sad_u8 (+ v_sad_hi_u8) per 4 columns, the R bytes packed from the staged entries
     // (r = 5: 18 -> 15 chain steps, r = 7: 22 -> 16).
-#ifndef USV_PAIR_JUMP
-#define USV_PAIR_JUMP 1
-#endif
     static constexpr int JA = K - 1;                                  // first increment in a quad
-    static constexpr int JN = USV_PAIR_JUMP ? (WIN - K + 1) / 4 : 0;  // quads
+    static constexpr int JN = (WIN - K + 1) / 4;                      // quads
     static constexpr int JE = JA + 4 * JN;                            // singles resume here
-    static constexpr int PD = USV_PAIR_PD > 0 && USV_PAIR_PD < NB ? USV_PAIR_PD : NB - 1;
+    static constexpr int PD = NB - 1;  // rows of DMA look-ahead
     static constexpr int KRB = WIN;
     static constexpr int RBUF_OFF = 0;
     static constexpr int TB_OFF = RBUF_OFF + NW * NB * NRS;
@@ -92,14 +72,11 @@ struct PCfg {
     // alternate two buffers so a flush needs one barrier
     static constexpr int NCB = NW == 1 ? 1 : 2;
     static constexpr int LUT_OFF = COMB_OFF + NCB * KRB * NW * K;
-#ifndef USV_PAIR_LDS_PAD
-#define USV_PAIR_LDS_PAD 0  // probe: extra LDS words per workgroup
-#endif
     // distance table in LDS: one wave means D <= 128, so every output disparity is < 128 and half the
     // table suffices (1 KB less: the static ring's 12 workgroups per CU fit only below ~12.5 KB each,
     // profiles/probes_r04/lds_residency_r04.txt)
     static constexpr int LUTN = NW == 1 ? 128 : 256;
-    static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN + USV_PAIR_LDS_PAD;
+    static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN;
     static_assert(RAD >= 2 && RAD <= 7, "paired kernel: 5 <= w <= 15");
     static_assert(PD * NQ < 64, "look-ahead DMAs must fit the 6-bit vmcnt");
     static_assert(NQ <= 5, "dma_row_buf issues at most 5 DMAs");
@@ -319,9 +296,9 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         };
         auto chain_step = [&](auto jt) {
             constexpr int j = decltype(jt)::value;
-            // the pairs this op needs that no earlier op waited for; retired USV_PAIR_RDASM_GRP at a time
+            // the pairs this op needs that no earlier op waited for, retired by one counted wait
             // (a group never spans the two read batches of r = 7)
-            constexpr int GRP = USV_PAIR_RDASM_GRP;
+            constexpr int GRP = 1;
             constexpr int kp = j == 0 ? -1 : need(j - 1) / 2;  // pairs [0, kp] already retired
             constexpr int kn = need(j) / 2;                    // pairs [0, kn] needed now
             if constexpr (RDASM && is_op(j) && kn > kp) {
@@ -405,12 +382,12 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     };
 
     int cb = 0, y_chunk = y_begin;
-    // Wide flush (USV_WIDE_FLUSH): a chunk's outputs leave in two store instructions -- lane r
+    // Wide flush: a chunk's outputs leave in two store instructions -- lane r
     // writes row r's 8 disparity bytes as one 8-byte store, lane 4r + q row r's distances 2q, 2q+1
     // as one 16-byte store -- instead of a byte + a double per lane and item (4 per 11-row chunk).
     // Global stores count in vmcnt on gfx9 with the LDS-DMA look-ahead, so fewer, wider stores also
     // hold up fewer of the next rows' counted DMA waits.  Needs 4-byte aligned disparity rows.
-    const bool wide = USV_WIDE_FLUSH && ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
+    const bool wide = ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
     auto flush = [&](int rows) {
         if constexpr (NW > 1) lds_barrier();
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
@@ -476,7 +453,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     // M0 = rbase + 4 ((I + PD) mod NB) NRS -- nothing in between writes M0 -- so the stores address tb from it)
     auto tr_issue = [&](const uint32_t(&S)[K], auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
-        constexpr bool REUSE = USV_PAIR_M0REUSE && USV_PAIR_ADDTID && C::STATIC && kPairPipe<RAD> && NW == 1;
+        constexpr bool REUSE = USV_PAIR_M0REUSE && C::STATIC && kPairPipe<RAD> && NW == 1;
         if constexpr (REUSE) {
             static_assert(K == 8 && C::TB_OFF >= NB * C::NRS, "eight transpose stores above the ring");
             constexpr uint32_t D0 = 4u * (uint32_t)(C::TB_OFF - ((I + PD) % NB) * C::NRS);
@@ -488,7 +465,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                          :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
                             "n"(D0), "n"(D0 + 256u), "n"(D0 + 512u), "n"(D0 + 768u), "n"(D0 + 1024u), "n"(D0 + 1280u),
                             "n"(D0 + 1536u), "n"(D0 + 1792u) : "memory");
-        } else if constexpr (USV_PAIR_ADDTID) {
+        } else {
             // ds_write_addtid_b32: address = M0 + offset + 4 lane, no address VGPR; 2 LDS cycles per store
             // against 6 for each ds_write2st64_b32 pair (MI355X_MICROARCH.md LDS table)
             static_assert(K == 8, "eight transpose stores");
@@ -499,9 +476,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                          "ds_write_addtid_b32 %6 offset:1536\n\tds_write_addtid_b32 %7 offset:1792"
                          :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
                             "s"(tb_lds) : "memory", "m0");
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
         }
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -730,18 +704,15 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     const long NC = (long)P.n_xt * a.batch;
     long m = slots / NC;
     if (m < 1) m = 1;
-    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    const long m_max = a.H / (kMinBandWins * WIN) > 0 ? a.H / (kMinBandWins * WIN) : 1;
     if (m > m_max) m = m_max;
     P.m = (int)m;
     const long ex = slots - NC * m;
-    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && ex > 0 && ex < P.n_xt &&
-               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= kMinBandWins * WIN) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
-#ifndef USV_PAIR_GEN_G_X4
-#define USV_PAIR_GEN_G_X4 4  // experiment knob: generation size x4/4 (4 = one generation per SIMD-wave slot)
-#endif
-    P.gen_g = (int)((4L * (cu_count() / 8)) * USV_PAIR_GEN_G_X4 / (4 * NW));
+    P.gen_g = (int)((4L * (cu_count() / 8)) / NW);  // one generation = one workgroup per SIMD-wave slot
     if (P.gen_g < 1) P.gen_g = 1;
     const bool three = per_cu * NW == 12 && total > 2L * 8 * P.gen_g;
     P.weights = !three ? 0x01010101u
@@ -753,16 +724,8 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifndef USV_PAIR
-#define USV_PAIR 1  // paired-disparity kernel for D > 64 (even D, 11 <= w <= 15)
-#endif
-#ifndef USV_PAIR_SMALL
-#define USV_PAIR_SMALL 0  // experiment: the paired kernel also for even 32 < D <= 64 and 5 <= w <= 9
-#endif
-bool pair_supported(const MatchArgs& a) {
-    if (USV_PAIR_SMALL && a.D > 32 && a.D <= 64 && (a.D % 2) == 0 && a.w >= 5 && a.w <= 9) return true;
-    return USV_PAIR && a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15;
-}
+// the paired-disparity kernel: even D > 64, 11 <= w <= 15 (smaller D take the grouped kernel, usv_sad_group.hip)
+bool pair_supported(const MatchArgs& a) { return a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15; }
 template <int RAD>
 hipError_t launch_pair_r(const MatchArgs& a, hipStream_t s) {
     return a.D <= 128 ? launch_pair_rn<RAD, 1>(a, s) : launch_pair_rn<RAD, 2>(a, s);
@@ -775,11 +738,6 @@ bool pair_path_supported(const MatchArgs& a) { return pair_supported(a); }
 hipError_t launch_pair(const MatchArgs& a, hipStream_t s) {
     if (!pair_supported(a)) return hipErrorInvalidValue;
     switch ((a.w - 1) / 2) {
-#if USV_PAIR_SMALL
-        case 2: return launch_pair_r<2>(a, s);
-        case 3: return launch_pair_r<3>(a, s);
-        case 4: return launch_pair_r<4>(a, s);
-#endif
         case 5: return launch_pair_r<5>(a, s);
         case 6: return launch_pair_r<6>(a, s);
         case 7: return launch_pair_r<7>(a, s);

@@ -454,12 +454,12 @@ hipError_t launch_ssd_rn(const MatchArgs& a, hipStream_t s) {
     const long NC = (long)P.n_xt * a.batch;
     long m = slots / NC;
     if (m < 1) m = 1;
-    const long m_max = a.H / (USV_MIN_BAND_WINS * WIN) > 0 ? a.H / (USV_MIN_BAND_WINS * WIN) : 1;
+    const long m_max = a.H / (kMinBandWins * WIN) > 0 ? a.H / (kMinBandWins * WIN) : 1;
     if (m > m_max) m = m_max;
     P.m = (int)m;
     const long ex = slots - NC * m;
-    P.extra = (USV_EXTRA_BANDS && a.batch == 1 && ex > 0 && ex < P.n_xt &&
-               a.H / (m + 1) >= USV_MIN_BAND_WINS * WIN) ? (int)ex : 0;
+    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt &&
+               a.H / (m + 1) >= kMinBandWins * WIN) ? (int)ex : 0;
     const long total = NC * m + P.extra;
     if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
     P.gen_g = (int)((4L * (cu_count() / 8)) / NW);

@@ -76,9 +76,6 @@ __host__ __device__ constexpr uint64_t row_gt_col_mask(int r) {
     return m;
 }
 
-#ifndef USV_SSD_MFMA_ORDER
-#define USV_SSD_MFMA_ORDER 0  // 1: all MFMA chains of a block before its epilogues (more VGPRs)
-#endif
 #ifndef USV_SSD_MFMA_OCC
 #define USV_SSD_MFMA_OCC 3  // waves per SIMD the kernel is compiled for
 #endif
@@ -243,26 +240,15 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
             mi32x4 Tv[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) Tv[g] = Tb[2 * g];  // rows 8 g + 4 h .. + 3 of the block
-            // USV_SSD_MFMA_ORDER 1: both sub-tiles' MFMA chains first, then the epilogues (the matrix pipe runs
-            // sub-tile 1's chain while the VALU reduces sub-tile 0's block; two accumulators live)
-            mi32x16 accs[NS];
-            auto chain = [&](int t) {
+            // (each sub-tile's MFMA chain right before its epilogue: both chains first, so the matrix pipe runs
+            // one while the VALU reduces the other, needs two live accumulators -- 242 VGPRs or spills, slower)
+#pragma unroll
+            for (int t = 0; t < NS; ++t) {
+                if (b < t || b > t + DB) continue;
                 mi32x16 acc = {};
 #pragma unroll
                 for (int s = 0; s < NSTEP; ++s)
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aop[s], Bop[t][s], acc, 0, 0, 0);
-                accs[t] = acc;
-            };
-            if constexpr (USV_SSD_MFMA_ORDER == 1) {
-#pragma unroll
-                for (int t = 0; t < NS; ++t)
-                    if (b >= t && b <= t + DB) chain(t);
-            }
-#pragma unroll
-            for (int t = 0; t < NS; ++t) {
-                if (b < t || b > t + DB) continue;
-                if constexpr (USV_SSD_MFMA_ORDER != 1) chain(t);
-                const mi32x16 acc = accs[t];
                 int k[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) k[r] = (acc[r] << 9) + Tv[r >> 2][r & 3];  // -key: one v_lshl_add_u32
