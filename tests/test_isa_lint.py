@@ -369,3 +369,14 @@ def test_tiled_lds_dma_m0_wait_state(tiled_kernels):
 def test_tiled_no_sgpr_use_while_scalar_load_in_flight(tiled_kernels):
     bad = {k: inflight_scalar_load_hazards(v)[:3] for k, v in tiled_kernels.items()}
     assert not any(bad.values()), {k: v for k, v in bad.items() if v}
+
+
+def test_mfma_kernel_has_no_inline_asm_valu():
+    # The compiler pads the MFMA wait states of its own instructions, not those of inline asm.  In round 5 a
+    # variant of the SSD matrix kernel whose sel_mask() selects (inline-asm v_cndmask) were scheduled into an
+    # MFMA's shadow wrote an operand register the MFMA was still reading and produced wrong maps; the product
+    # kernel's selects are plain C++ since.  Keep every VALU of the MFMA kernel compiler-visible.
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "unsynchronized_stereo_vision_proj325_amd", "csrc", "usv_ssd_mfma.hip")).read()
+    code = "\n".join(line.split("//")[0] for line in src.splitlines())
+    assert "sel_mask(" not in code and "asm" not in code

@@ -55,6 +55,20 @@ def test_matrix_ssd_shapes(gpu, W, H, D, w):
     assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
 
 
+@pytest.mark.parametrize("w", [3, 5, 7, 9, 11])
+@pytest.mark.parametrize("D", [32, 64, 96, 128, 160])
+def test_matrix_ssd_every_instantiation(gpu, w, D):
+    """Every (w, D) the kernel is instantiated for (ssd_mfma_kernel<(w - 1) / 2, D / 32>), each compiled
+    separately (its own register allocation and schedule), on a frame with border tiles on both sides."""
+    rng = np.random.default_rng(w * 1000 + D)
+    H, W = 28, 232
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = np.roll(L, 9, axis=1) ^ rng.integers(0, 4, (H, W), dtype=np.uint8)
+    ref = oracle_sad(L, R, D, w, "ssd", "naive")
+    got = _run(gpu, L, R, D, w)
+    assert np.array_equal(got, ref), (w, D, _mismatch(got, ref))
+
+
 @pytest.mark.parametrize("levels", [2, 4, 64])
 def test_matrix_ssd_ties(gpu, levels):
     """Low-entropy images (2, 4 or 64 grey levels): many equal costs, the smallest d must win every tie."""

@@ -68,14 +68,6 @@ struct MCfg {
     static_assert(WIN <= 15, "the window's rows and the one leaving fit the 16-slot ring");
 };
 
-// lanes whose C row of register r lies below their column index: (lane & 31) < (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-__host__ __device__ constexpr uint64_t row_gt_col_mask(int r) {
-    uint64_t m = 0;
-    for (int l = 0; l < 64; ++l)
-        if ((l & 31) < (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) m |= 1ull << l;
-    return m;
-}
-
 #ifndef USV_SSD_MFMA_OCC
 #define USV_SSD_MFMA_OCC 3  // waves per SIMD the kernel is compiled for
 #endif
@@ -208,6 +200,11 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
     const mi32x4* recR = reinterpret_cast<const mi32x4*>(smem + C::R_OFF);
     const mi32x4* recL = reinterpret_cast<const mi32x4*>(smem + C::L_OFF);
 
+    // the edge blocks' valid-d lane masks, one per accumulator register r (C row (r & 3) + 8 (r >> 2) + 4 h against
+    // column j), computed once: loop-invariant lane masks the selects below read from SGPRs
+    bool below[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) below[r] = j < (r & 3) + 8 * (r >> 2) + 4 * h;
     for (int y = y_begin; y < y_end; ++y) {
         // L: row y + r enters the window, row y - r - 1 left; R: row y + 1 + r for the next row's table
         if (y > y_begin) put_l(y - RAD - 1, kClearL);
@@ -254,10 +251,10 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
                 for (int r = 0; r < 16; ++r) k[r] = (acc[r] << 9) + Tv[r >> 2][r & 3];  // -key: one v_lshl_add_u32
                 if (b == t) {  // d = D + j - i: valid for j < i
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) k[r] = (int)sel_mask(0x80000000u, (uint32_t)k[r], row_gt_col_mask(r));
+                    for (int r = 0; r < 16; ++r) k[r] = below[r] ? k[r] : (int)0x80000000u;
                 } else if (b == t + DB) {  // d = j - i: valid for j >= i
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) k[r] = (int)sel_mask((uint32_t)k[r], 0x80000000u, row_gt_col_mask(r));
+                    for (int r = 0; r < 16; ++r) k[r] = below[r] ? (int)0x80000000u : k[r];
                 }
                 int m = run[t];
 #pragma unroll
@@ -268,7 +265,10 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
         // a column's rows are split over the two half-waves: combine; lane (j, h) writes sub-tile h's column j
 #pragma unroll
         for (int t = 0; t < NS; ++t) run[t] = max(run[t], __shfl_xor(run[t], 32, 64));
-        const int key = -(int)sel_mask((uint32_t)run[0], (uint32_t)run[1], 0xFFFFFFFF00000000ull);
+        // (every select in this kernel is compiler-visible C++, not sel_mask()'s inline asm: the compiler pads the
+        // MFMA wait states of its own instructions only, and an asm select placed in an MFMA's shadow by the
+        // scheduler wrote an operand register the MFMA was still reading -- tests/test_isa_lint.py checks)
+        const int key = -(h ? run[1] : run[0]);
         const int d = 32 * h + j + D - 255 + (key & 0xFF);
         const int x = x0 + 32 * h + j;
         disp[(size_t)y * a.disp_pitch + x] = (uint8_t)d;
