@@ -140,6 +140,21 @@ usv_status usv_sad_disparity_batch(const uint8_t* L, const uint8_t* R, int batch
                                    int disp_pitch, double* dist_cm, size_t dist_stride,
                                    int dist_pitch, const double* lut_cm, void* stream);
 
+/* A prepared match for a caller that repeats the same match over the same buffers (a frame loop into
+ * fixed device buffers): usv_match_plan_create takes usv_sad_disparity_batch's arguments plus the kernel
+ * choice (kernel != USV_KERNEL_AUTO needs batch == 1), validates them, resolves the distance table and
+ * the kernel once, and returns a plan; usv_match_plan_launch enqueues one match on the plan's stream with
+ * no further checks (one pointer argument: the per-call host cost is the launch itself).  The buffers and
+ * the stream must outlive the plan; a plan may be launched from one thread at a time.  Replaces nothing in
+ * the reference; it is the C side of StereoBlockMatcher.bind. */
+typedef struct usv_match_plan usv_match_plan;
+usv_status usv_match_plan_create(const uint8_t* L, const uint8_t* R, int batch, size_t pair_stride, int W, int H,
+                                 int pitch, int D, int w, int metric, uint8_t* disp, size_t disp_stride,
+                                 int disp_pitch, double* dist_cm, size_t dist_stride, int dist_pitch,
+                                 const double* lut_cm, int kernel, void* stream, usv_match_plan** out);
+usv_status usv_match_plan_launch(const usv_match_plan* plan);
+usv_status usv_match_plan_destroy(usv_match_plan* plan);
+
 /* ---- multi-GPU: one process, one device + stream + RCCL communicator per GPU ----
  *
  * SURVEY.md §8(b)(2) / §8(e).  A batch of independent frame pairs (configs D

@@ -70,6 +70,19 @@ def test_argument_validation_needs_no_gpu(usvlib):
     assert usvlib.usv_contour_pair_scores(p, 3, None, 2, p, None) == _lib.USV_ERR_INVALID_ARG
     assert usvlib.usv_contour_pair_scores(p, 3, p, 0, None, None) == _lib.USV_OK
     assert usvlib.usv_contour_pair_scores(p, 1 << 16, p, 1 << 16, p, None) == _lib.USV_ERR_UNSUPPORTED
+    # match plans: the same validation as usv_sad_disparity_batch, then nothing is allocated on failure
+    plan = ctypes.c_void_p(123)
+    args = [p, p, 1, 0, 64, 64, 64, 16, 5, 0, p, 0, 64, None, 0, 0, None]
+    assert usvlib.usv_match_plan_create(*args, 0, None, None) == _lib.USV_ERR_INVALID_ARG  # no out pointer
+    assert usvlib.usv_match_plan_create(*args[:7], 0, *args[8:], 0, None, ctypes.byref(plan)) == \
+        _lib.USV_ERR_UNSUPPORTED and plan.value is None  # D = 0
+    bad_batch = [p, p, 2, 64 * 64, 64, 64, 64, 16, 5, 0, p, 64 * 64, 64, None, 0, 0, None]
+    assert usvlib.usv_match_plan_create(*bad_batch, _lib.KERNEL_FAST, None, ctypes.byref(plan)) == \
+        _lib.USV_ERR_INVALID_ARG  # a batch takes the AUTO dispatch, as usv_sad_disparity_batch
+    assert usvlib.usv_match_plan_create(*args[:13], p, 0, 64, None, 0, None, ctypes.byref(plan)) == \
+        _lib.USV_ERR_INVALID_ARG  # distance map without a LUT
+    assert usvlib.usv_match_plan_launch(None) == _lib.USV_ERR_INVALID_ARG
+    assert usvlib.usv_match_plan_destroy(None) == _lib.USV_ERR_INVALID_ARG
 
 
 @pytest.mark.parametrize("model", ["moving_object", "canny"])

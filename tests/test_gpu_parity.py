@@ -545,3 +545,25 @@ def test_bound_launcher_matches_compute_and_oracle(gpu):
         m.bind(Lt, Rt[:, :320], out_disp=d1)
     with pytest.raises(ValueError):
         m.bind(Lt, Rt, out_disp=torch.zeros((200, 640), dtype=torch.int16, device=gpu))
+
+
+def test_bound_launcher_every_kernel_family(gpu):
+    # bind() runs a usv_match_plan (kernel resolved once at create): the SSD matrix kernel, the tiled kernel
+    # (W % 4 != 0), the grouped kernel (D = 64) and the direct-window kernel (w = 33) through the plan equal
+    # compute() on the same buffers; the plan stays valid across launches and is freed with the callable
+    rng = np.random.default_rng(17)
+    cases = [(256, 48, 128, 11, "ssd", "auto"), (250, 40, 64, 9, "sad", "auto"), (256, 40, 64, 7, "sad", "auto"),
+             (96, 40, 16, 33, "sad", "auto"), (256, 48, 96, 7, "ssd", "tiled")]
+    for W, H, D, w, metric, kernel in cases:
+        L = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(gpu)
+        R = torch.from_numpy(rng.integers(0, 256, (H, W), dtype=np.uint8)).to(gpu)
+        m = StereoBlockMatcher(D, w, metric, kernel=kernel)
+        ref = m.compute(L, R)
+        out = torch.zeros_like(L)
+        go = m.bind(L, R, out_disp=out)
+        out.zero_()
+        go()
+        go()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (W, H, D, w, metric, kernel)
+        del go

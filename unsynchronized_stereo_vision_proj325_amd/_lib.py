@@ -74,6 +74,11 @@ SIGNATURES = {
     "usv_sad_disparity_batch": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_void_p, c_size_t, c_int, c_void_p,
                                         c_size_t, c_int, c_void_p, c_void_p]),
+    "usv_match_plan_create": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, c_void_p, c_size_t, c_int, c_void_p, c_size_t, c_int, c_void_p,
+                                      c_int, c_void_p, POINTER(c_void_p)]),
+    "usv_match_plan_launch": (c_int, [c_void_p]),
+    "usv_match_plan_destroy": (c_int, [c_void_p]),
     "usv_shard_range": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
     "usv_shard_slot": (c_int, [c_int, c_int, c_int, c_int, POINTER(ctypes.c_longlong)]),
     "usv_batch_sharded_submit": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_size_t, c_int, c_void_p, c_void_p,

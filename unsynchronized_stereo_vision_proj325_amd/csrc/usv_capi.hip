@@ -107,7 +107,11 @@ usv_status validate(const usv::MatchArgs& a) {
     return USV_OK;
 }
 
-usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
+// Checks a match and resolves what every launch of it uses: the distance table's device address and the
+// concrete kernel (AUTO: SSD on the matrix cores where supported, else the fast kernels, else the tiled
+// sliding-window kernel -- any shape, w <= 31 -- else the direct-window kernel: w > 31, or a window too large
+// for the tiled ring).
+usv_status prepare(usv::MatchArgs& a, int& kernel) {
     usv_status st = validate(a);
     if (st != USV_OK) return st;
     if (kernel != USV_KERNEL_AUTO && kernel != USV_KERNEL_FAST && kernel != USV_KERNEL_GENERIC &&
@@ -117,35 +121,40 @@ usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
     if (kernel == USV_KERNEL_TILED && !usv::tiled_path_supported(a)) return USV_ERR_UNSUPPORTED;
     if (kernel == USV_KERNEL_MATRIX && !usv::ssd_mfma_supported(a)) return USV_ERR_UNSUPPORTED;
     if (a.dist && (st = resolve_lut(a.lut, &a.lut)) != USV_OK) return st;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (kernel == USV_KERNEL_AUTO)
+        kernel = usv::ssd_mfma_supported(a)      ? USV_KERNEL_MATRIX
+                 : usv::fast_path_supported(a)   ? USV_KERNEL_FAST
+                 : usv::tiled_path_supported(a)  ? USV_KERNEL_TILED
+                                                 : USV_KERNEL_GENERIC;
+    return USV_OK;
+}
+
+usv_status launch(const usv::MatchArgs& a, int kernel, hipStream_t s) {
     switch (kernel) {
-        case USV_KERNEL_AUTO:
-            // SSD on the matrix cores where supported, else the fast kernels, else the tiled sliding-window
-            // kernel (any shape, w <= 31), else the direct-window kernel (w > 31, or a window too large for the
-            // tiled ring)
-            if (usv::ssd_mfma_supported(a)) return to_status(usv::launch_ssd_mfma(a, s));
-            if (usv::fast_path_supported(a)) return to_status(usv::launch_fast(a, s));
-            if (usv::tiled_path_supported(a)) return to_status(usv::launch_tiled(a, s));
-            return to_status(usv::launch_generic(a, s));
-        case USV_KERNEL_FAST:
-            if (!usv::fast_path_supported(a)) return USV_ERR_UNSUPPORTED;
-            return to_status(usv::launch_fast(a, s));
-        case USV_KERNEL_TILED:
-            return to_status(usv::launch_tiled(a, s));
-        case USV_KERNEL_GENERIC:
-            return to_status(usv::launch_generic(a, s));
-        case USV_KERNEL_MATRIX:
-            return to_status(usv::launch_ssd_mfma(a, s));
-        default:
-            return USV_ERR_INVALID_ARG;
+        case USV_KERNEL_FAST: return to_status(usv::launch_fast(a, s));
+        case USV_KERNEL_TILED: return to_status(usv::launch_tiled(a, s));
+        case USV_KERNEL_GENERIC: return to_status(usv::launch_generic(a, s));
+        case USV_KERNEL_MATRIX: return to_status(usv::launch_ssd_mfma(a, s));
+        default: return USV_ERR_INVALID_ARG;
     }
+}
+
+usv_status dispatch(usv::MatchArgs a, int kernel, void* stream) {
+    const usv_status st = prepare(a, kernel);
+    return st != USV_OK ? st : launch(a, kernel, static_cast<hipStream_t>(stream));
 }
 
 }  // namespace
 
+struct usv_match_plan {
+    usv::MatchArgs a;
+    int kernel;  // concrete (never AUTO)
+    hipStream_t stream;
+};
+
 extern "C" {
 
-const char* usv_version(void) { return "usv-mi355x 0.4.1 (gfx950, " USV_BUILD_KIND ")"; }
+const char* usv_version(void) { return "usv-mi355x 0.4.2 (gfx950, " USV_BUILD_KIND ")"; }
 
 usv_status usv_device_check(int* n_devices) {
     int n = 0;
@@ -186,6 +195,34 @@ usv_status usv_sad_disparity_batch(const uint8_t* L, const uint8_t* R, int batch
     a.lut = lut_cm; a.batch = batch; a.pair_stride = pair_stride; a.disp_stride = disp_stride;
     a.dist_stride = dist_stride;
     return dispatch(a, USV_KERNEL_AUTO, stream);
+}
+
+usv_status usv_match_plan_create(const uint8_t* L, const uint8_t* R, int batch, size_t pair_stride, int W, int H,
+                                 int pitch, int D, int w, int metric, uint8_t* disp, size_t disp_stride,
+                                 int disp_pitch, double* dist_cm, size_t dist_stride, int dist_pitch,
+                                 const double* lut_cm, int kernel, void* stream, usv_match_plan** out) {
+    if (!out) return USV_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (batch > 1 && kernel != USV_KERNEL_AUTO) return USV_ERR_INVALID_ARG;  // as usv_sad_disparity_batch
+    usv::MatchArgs a{};
+    a.L = L; a.R = R; a.W = W; a.H = H; a.pitch = pitch; a.D = D; a.w = w; a.metric = metric;
+    a.disp = disp; a.disp_pitch = disp_pitch; a.dist = dist_cm; a.dist_pitch = dist_pitch;
+    a.lut = lut_cm; a.batch = batch; a.pair_stride = pair_stride; a.disp_stride = disp_stride;
+    a.dist_stride = dist_stride;
+    const usv_status st = prepare(a, kernel);
+    if (st != USV_OK) return st;
+    *out = new usv_match_plan{a, kernel, static_cast<hipStream_t>(stream)};
+    return USV_OK;
+}
+
+usv_status usv_match_plan_launch(const usv_match_plan* p) {
+    return p ? launch(p->a, p->kernel, p->stream) : USV_ERR_INVALID_ARG;
+}
+
+usv_status usv_match_plan_destroy(usv_match_plan* p) {
+    if (!p) return USV_ERR_INVALID_ARG;
+    delete p;
+    return USV_OK;
 }
 
 usv_status usv_disparity_to_distance(const uint8_t* disp, int W, int H, int disp_pitch,

@@ -166,43 +166,43 @@ class StereoBlockMatcher:
              out_dist: torch.Tensor | None = None, stream=None):
         """A zero-argument launcher for repeated matches over the same (resident) buffers.
 
-        Validates once -- the same checks and errors as compute() -- and returns a callable that enqueues
-        one match per call through the same C-ABI entry point (usv_sad_disparity_ex / _batch) with the
-        arguments already marshalled, so a caller stepping a frame stream from Python pays one ctypes
-        call per frame instead of compute()'s per-call validation (~10 us of host time per launch, more
-        than a whole 640x480 match).  The buffers must stay alive (and unmoved) while the callable is used.
+        Validates once -- the same checks and errors as compute(), plus one real match through compute() --
+        then prepares a usv_match_plan (include/usv.h: arguments checked, distance table and kernel resolved
+        once) and returns a callable that enqueues one match per call with usv_match_plan_launch: one
+        pointer argument, so a caller stepping a frame stream from Python pays the launch itself instead of
+        compute()'s per-call validation and argument marshalling.  The buffers must stay alive (and
+        unmoved) while the callable is used; the plan is freed with the callable.
         """
+        import weakref
+
         with_distance = out_dist is not None
         self.compute(left, right, with_distance=with_distance, out_disp=out_disp, out_dist=out_dist,
                      stream=stream)  # validation + one real launch (raises exactly as compute() does)
         lib = _lib.load()
         with torch.cuda.device(left.device):
             s = _stream(stream)
-        lut = self.lut_device(left.device) if with_distance else None
-        H, W = left.shape[-2], left.shape[-1]
-        pitch = left.stride(-2)
-        dist_args = ((out_dist.data_ptr(), out_dist.stride(-2), lut.data_ptr()) if with_distance
-                     else (None, 0, None))
-        if left.dim() == 2:
-            fn, name = lib.usv_sad_disparity_ex, "usv_sad_disparity_ex"
-            args = (left.data_ptr(), right.data_ptr(), W, H, pitch, self.num_disparities, self.window,
-                    _METRICS[self.metric], out_disp.data_ptr(), out_disp.stride(-2), *dist_args,
-                    _KERNELS[self.kernel], s)
-        else:
-            fn, name = lib.usv_sad_disparity_batch, "usv_sad_disparity_batch"
-            args = (left.data_ptr(), right.data_ptr(), left.shape[0], left.stride(0), W, H, pitch,
-                    self.num_disparities, self.window, _METRICS[self.metric], out_disp.data_ptr(),
-                    out_disp.stride(0), out_disp.stride(-2), dist_args[0],
-                    out_dist.stride(0) if with_distance else 0, dist_args[1], dist_args[2], s)
+            lut = self.lut_device(left.device) if with_distance else None
+            batched = left.dim() == 3
+            H, W = left.shape[-2], left.shape[-1]
+            plan = ctypes.c_void_p()
+            _lib.check("usv_match_plan_create", lib.usv_match_plan_create(
+                left.data_ptr(), right.data_ptr(), left.shape[0] if batched else 1, left.stride(0) if batched else 0,
+                W, H, left.stride(-2), self.num_disparities, self.window, _METRICS[self.metric],
+                out_disp.data_ptr(), out_disp.stride(0) if batched else 0, out_disp.stride(-2),
+                out_dist.data_ptr() if with_distance else None,
+                out_dist.stride(0) if (with_distance and batched) else 0,
+                out_dist.stride(-2) if with_distance else 0, lut.data_ptr() if with_distance else None,
+                _KERNELS[self.kernel] if not batched else _lib.KERNEL_AUTO, s, ctypes.byref(plan)))
         keep = (left, right, out_disp, out_dist, lut)  # the callable holds its buffers alive
-        check = _lib.check
+        fn, handle, check = lib.usv_match_plan_launch, plan.value, _lib.check
 
         def launch():
-            st = fn(*args)
+            st = fn(handle)
             if st:
-                check(name, st)
+                check("usv_match_plan_launch", st)
             return keep[2]
 
+        weakref.finalize(launch, lib.usv_match_plan_destroy, handle)
         return launch
 
 
