@@ -869,6 +869,8 @@ def main():
     launch = [matcher.bind(Lt, Rt, out_disp=disp_bufs[b][0, :rows], out_dist=dist_bufs[b] if with_dist else None,
                            stream=streams[b % len(streams)]) for b in range(nbuf)]
 
+    gathers = world > 1 and a.gather != "none"
+
     def step(i):
         b = i % nbuf
         if pending[b] is not None:  # the gather that last read this buffer must finish first
@@ -876,8 +878,9 @@ def main():
                 pending[b].wait()
             pending[b] = None
         launch[b]()
-        with torch.cuda.stream(streams[b % len(streams)]):  # the gather is ordered behind this frame only
-            collect(b)
+        if gathers:
+            with torch.cuda.stream(streams[b % len(streams)]):  # the gather is ordered behind this frame only
+                collect(b)
 
     def collect(b):
         if bands and a.gather != "none":
