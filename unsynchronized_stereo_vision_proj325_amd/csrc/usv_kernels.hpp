@@ -12,14 +12,14 @@
 // included before any knob's default is defined, so a knob set on the command line of a product
 // build is an error here.
 #ifndef USV_VARIANT_BUILD
-#if defined(USV_GEN_WEIGHTS) || defined(USV_GROUP_LDSR) || defined(USV_GROUP_MIN_BAND_ROWS) ||                   \
-    defined(USV_GROUP_MIN_BAND_WINS) || defined(USV_GROUP_OCC) || defined(USV_GROUP_WEIGHTS) ||                  \
-    defined(USV_HIST_KU) || defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_NW2) ||                \
+#if defined(USV_GEN_WEIGHTS) || defined(USV_GROUP_MIN_BAND_ROWS) || defined(USV_GROUP_MIN_BAND_WINS) ||          \
+    defined(USV_GROUP_OCC) || defined(USV_GROUP_WEIGHTS) || defined(USV_HIST_KU) ||                              \
+    defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_NW2) ||                                        \
     defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) || defined(USV_PAIR_M0REUSE) || defined(USV_PAIR_OCC5) ||              \
     defined(USV_PAIR_OCC7) || defined(USV_PAIR_RDASM) || defined(USV_PREP_KU) || defined(USV_PREP_THREADS) ||    \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_SSD_GEN_WEIGHTS) ||                        \
-    defined(USV_SSD_LDSR) || defined(USV_SSD_MFMA_MINROWS) || defined(USV_SSD_MFMA_OCC) ||                       \
-    defined(USV_SSD_MFMA_WAVES) || defined(USV_STAMPS) || defined(USV_WGTIME)
+    defined(USV_SSD_MFMA_MINROWS) || defined(USV_SSD_MFMA_OCC) || defined(USV_SSD_MFMA_WAVES) ||                 \
+    defined(USV_STAMPS) || defined(USV_WGTIME)
 #error "tuning knobs are variant-build only: use scripts/build_variant.sh (it defines USV_VARIANT_BUILD)"
 #endif
 #define USV_BUILD_KIND "product build"

@@ -80,9 +80,7 @@ __device__ __forceinline__ void dma_row_lr(gsu4 rsrcR, gsu4 rsrcL, uint32_t soff
 // ds_read_b64 / ds_read_b128 issued by inline asm in order of first use, each retired by a counted lgkmcnt
 // wait before the chain step that first needs it (the compiler pairs plain 8-byte reads into ds_read2_b64,
 // 8 cycles per pair against 2 per single read), and the argmin transpose stores as ds_write_addtid_b32.
-#ifndef USV_GROUP_LDSR
-#define USV_GROUP_LDSR 1  // rocprof A/B: B 10.62 -> 10.34 us, A 5.78 -> 5.70 us
-#endif
+// (these forms: rocprof A/B B 10.62 -> 10.34 us, A 5.78 -> 5.70 us, round 4)
 typedef uint32_t gu2 __attribute__((ext_vector_type(2)));
 template <uint32_t OFF>
 __device__ __forceinline__ void g_ds_read_b64(gu2& v, uint32_t addr) {
@@ -123,7 +121,7 @@ struct GCfg {
     static_assert(NE_V + 2 * (PP - 1) + K * (G - 1) <= NQ * 64, "a lane's entries stay inside the R part");
     static_assert(NL_V + K * (G - 1) <= 64, "a lane's L entries stay inside the L part");
     static_assert(PD * NDMA < 64, "look-ahead DMAs fit the 6-bit vmcnt");
-    // asm read schedule (USV_GROUP_LDSR): NEP b64 R pairs (pair k first used by chain step k ? 2k - 1 : 0),
+    // asm read schedule: NEP b64 R pairs (pair k first used by chain step k ? 2k - 1 : 0),
     // NLQ b128 L quads (quad m first used by step 4m), issued in order of first use (L first on ties)
     static constexpr int NEP = NE_V / 2, NLQ = NL_V / 4, NRD = NEP + NLQ;
     static constexpr int first_use(int code) { return code >= 64 ? 4 * (code - 64) : (code == 0 ? 0 : 2 * code - 1); }
@@ -220,7 +218,7 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
         uint32_t Lv[C::NL_V], E[C::NE_V];
         gu2 ev[C::NEP];
         gsu4 lv[C::NLQ];
-        if constexpr (USV_GROUP_LDSR) {
+        {
             const uint32_t sa = g_lds_addr(slot);
             const uint32_t ra = sa + 4u * (uint32_t)s_r, la = sa + 4u * (uint32_t)s_lv;
             [&]<int... N>(std::integer_sequence<int, N...>) {
@@ -231,24 +229,10 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
                 };
                 (one(std::integral_constant<int, N>{}), ...);
             }(std::make_integer_sequence<int, C::NRD>{});
-        } else {
-            const uint4* lq = reinterpret_cast<const uint4*>(slot + s_lv);
-#pragma unroll
-            for (int k = 0; k < C::NL_V / 4; ++k) {
-                const uint4 v = lq[k];
-                Lv[4 * k] = v.x; Lv[4 * k + 1] = v.y; Lv[4 * k + 2] = v.z; Lv[4 * k + 3] = v.w;
-            }
-            const uint2* rq = reinterpret_cast<const uint2*>(slot + s_r);
-#pragma unroll
-            for (int k = 0; k < C::NE_V / 2; ++k) {
-                const uint2 v = rq[k];
-                E[2 * k] = v.x;
-                E[2 * k + 1] = v.y;
-            }
         }
         uint32_t A[NPOS + 1];
         A[0] = 0;
-        if constexpr (USV_GROUP_LDSR) {
+        {
             auto step_j = [&](auto jt) {
                 constexpr int j = decltype(jt)::value;
                 constexpr int have = j == 0 ? 0 : C::needed(j - 1), need = C::needed(j);
@@ -279,10 +263,6 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
                 (step_j(std::integral_constant<int, J>{}), ...);
             }(std::make_integer_sequence<int, NPOS>{});
             static_assert(C::needed(NPOS - 1) == C::NRD, "every read retired by the last step");
-        } else {
-#pragma unroll
-            for (int j = 0; j < NPOS; ++j)
-                A[j + 1] = __builtin_amdgcn_sad_hi_u8(Lv[j], E[j], __builtin_amdgcn_sad_u8(Lv[j], E[j + 1], A[j]));
         }
 #pragma unroll
         for (int x = 0; x < K; ++x) {
@@ -332,7 +312,7 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
     };
     const uint32_t tb_lds = g_lds_addr(tb);
     auto emit = [&](const uint32_t(&S)[K], int slot_row) {
-        if constexpr (USV_GROUP_LDSR) {
+        {
             static_assert(K == 8, "eight transpose stores");
             asm volatile("s_mov_b32 m0, %8\n\ts_nop 0\n\t"
                          "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:256\n\t"
@@ -341,9 +321,6 @@ __device__ __forceinline__ void group_band_loop(const uint8_t* __restrict__ L, c
                          "ds_write_addtid_b32 %6 offset:1536\n\tds_write_addtid_b32 %7 offset:1792"
                          :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
                             "s"(tb_lds) : "memory", "m0");
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) tb[64 * i + lane] = S[i];
         }
         asm volatile("" ::: "memory");
         uint4 w2[2];

@@ -23,12 +23,9 @@ namespace {
 //     steps.  Ties -> smallest d, as in the SAD kernels.
 // Integer arithmetic only: bit-exact with oracle/sad_oracle.c's SSD by construction.
 // ===================================================================================
-// LDS-cycle forms of the paired kernel (usv_sad_pair.hip), USV_SSD_LDSR: the staged
+// LDS-cycle forms of the paired kernel (usv_sad_pair.hip; config C SSD 108.0 -> 102.3 us): the staged
 // entries as single ds_read_b64 issued by inline asm with a counted wait before the first chain step that needs
 // each pair (the compiler pairs plain reads into ds_read2_b64), the transpose stores as ds_write_addtid_b32.
-#ifndef USV_SSD_LDSR
-#define USV_SSD_LDSR 1  // rocprof: config C SSD 108.0 -> 102.3 us
-#endif
 typedef uint32_t ssd_u2 __attribute__((ext_vector_type(2)));
 typedef uint32_t ssd_u4 __attribute__((ext_vector_type(4)));
 template <uint32_t OFF>
@@ -170,7 +167,7 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
         asm volatile("" : "+s"(boff));
         const VT* rb = reinterpret_cast<const VT*>(rbuf + boff + s_l);
         uint32_t E[C::NPOS_V];
-        constexpr bool LDSR = USV_SSD_LDSR && C::VEC == 2;
+        constexpr bool LDSR = C::VEC == 2;
         constexpr int NV = C::NPOS_V / 2;
         ssd_u2 ev[NV];
         if constexpr (LDSR) {
@@ -282,7 +279,7 @@ __device__ __forceinline__ void ssd_band_loop(const uint8_t* __restrict__ L, con
     };
     const uint32_t tb_lds = lds_addr(tb);
     auto tr_issue = [&](const uint32_t(&S)[K]) {
-        if constexpr (USV_SSD_LDSR && C::VEC == 2) {  // (NW = 1, 4: more VGPRs, a spill at r = 5, NW = 4)
+        if constexpr (C::VEC == 2) {  // (NW = 1, 4: more VGPRs, a spill at r = 5, NW = 4)
             static_assert(K == 8, "eight transpose stores");
             asm volatile("s_mov_b32 m0, %8\n\ts_nop 0\n\t"
                          "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:256\n\t"
