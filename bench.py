@@ -795,7 +795,7 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     ssd = StereoBlockMatcher(D, w, "ssd", kernel="matrix")
     us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s, preload="self")
     out["ssd_matrix"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6),
-                         "kernel": "ssd_mfma_kernel (v_mfma_i32_32x32x32_i8)",
+                         "kernel": "ssd_mfma_kernel (v_mfma_i32_16x16x64_i8)",
                          "mfma_tops": 2.0 * 32 * 32 * 32 * (60 * H * ((W + 63) // 64)) / (us * 1e-6) / 1e12}
     for kernel, n in (("tiled", steps * 8), ("generic", steps)):
         ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)

@@ -1,6 +1,6 @@
 """GPU parity of the matrix-core SSD kernel (csrc/usv_ssd_mfma.hip, kernel="matrix") against the CPU oracle.
 
-The kernel computes the window cross term Σ a'b' with v_mfma_i32_32x32x32_i8 and the argmin over SB - 2C
+The kernel computes the window cross term Σ a'b' with v_mfma_i32_16x16x64_i8 and the argmin over SB - 2C
 (SSD variant; oracle/sad_oracle.c).  Integer arithmetic, so the disparity maps must be
 bit-identical to the oracle's, ties (smallest d) and replicate borders included, and the fused distance map
 bit-identical to the table gather.

@@ -1,5 +1,5 @@
 // usv_ssd_mfma.hip -- SSD block match with the window's cross term on the gfx950 matrix cores
-// (ssd_mfma_kernel: v_mfma_i32_32x32x32_i8; w <= 11, D a multiple of 32 up to 160).
+// (ssd_mfma_kernel: v_mfma_i32_16x16x64_i8; w <= 11, D a multiple of 32 up to 160).
 //
 // Spec: SURVEY.md §8(a) A1, SSD variant (restated in oracle/sad_oracle.c).  With a' = a - 128 and b' = b - 128
 // (signed bytes, exact: a' = (int8)(a ^ 0x80)), for output pixel x, disparity d and R window centre m = x - d:
@@ -10,30 +10,36 @@
 //   C[m][x] = Σ_k A[m][k] B[k][x],   A[m][k] = b'(row, m - r + dx),   B[k][x] = a'(row, x - r + dx).
 //
 // Operands come from COLUMN RECORDS: the LDS holds, per staged column, 16 bytes = the column's value in the 16
-// slots of a row ring (row ρ in byte ρ & 15), holding exactly the current window's rows and zero elsewhere (a row
-// is written when it enters the window and zeroed when it leaves).  A K-step of v_mfma_i32_32x32x32_i8 is then two
-// window columns (dx = 2 s + h for lane half h) x the 16 ring slots: lane (i, h) of the A operand is the record of
-// R column m_i - r + dx, lane (j, h) of B the record of L column x_j - r + dx -- one aligned ds_read_b128 each,
-// the same byte order (ring slot) in both, so the k order inside a step is the same permutation of window rows
-// for A and B, which the sum does not see (profiles/probes_r05/mfma_i8_layout_r05.txt: any consistent k order
-// gives the product).  dx >= w reads a zero record.  Unaligned LDS reads are exact on gfx950 but serialise
-// (255 vs 39 cycles per wave-instruction, profiles/probes_r05/lds_unaligned_r05.txt): records keep every read
-// 16-byte aligned, and the ring needs no im2col copy per output row.
+// slots of a row ring (row ρ in byte ρ & 15).  The L records hold exactly the current window's rows and zero
+// elsewhere (a row is written when it enters the window and zeroed when it leaves).  A K-step of
+// v_mfma_i32_16x16x64_i8 is four window columns (dx = 4 s + g for lane group g = lane >> 4) x the 16 ring slots:
+// lane (i, g) of the A operand is the record of R column m_i - r + dx, lane (j, g) of B the record of L column
+// x_j - r + dx -- one aligned ds_read_b128 each, the same byte order (ring slot) in both, so the k order inside a
+// step is the same permutation of window rows for A and B, which the sum does not see
+// (profiles/probes_r05/mfma_i8_layout_r05.txt: any consistent k order gives the product).  dx >= w reads a zero
+// record.  Unaligned LDS reads are exact on gfx950 but serialise (255 vs 39 cycles per wave-instruction,
+// profiles/probes_r05/lds_unaligned_r05.txt): records keep every read 16-byte aligned, and the ring needs no
+// im2col copy per output row.
 //
-// A wave owns XT = 64 output columns (two 32-column sub-tiles t) and a band of rows.  Sub-tile t's R centres run
-// over m-blocks b = t .. t + D/32 of the wave's NBM = 2 + D/32 blocks of 32 from m_lo = x0 - D; block b = t holds
-// d = D + j - i (valid for j < i), block t + D/32 holds d = j - i (valid for j >= i), the blocks between are all
-// valid (i: the block's m row, j: the sub-tile's x column).  Per output row:
+// A wave owns XT = 64 output columns (four 16-column sub-tiles t) and a band of rows.  Sub-tile t's R centres run
+// over m-blocks b = t .. t + D/16 of the wave's NBM = 4 + D/16 blocks of 16 from m_lo = x0 - D; block b = t holds
+// d = D + j - i (valid for j < i), block t + D/16 holds d = j - i (valid for j >= i), the blocks between are all
+// valid (i: the block's m row, j: the sub-tile's x column).  16-row blocks make the two triangular edge blocks
+// 2 of D/16 + 1 per sub-tile (of D/32 + 1 with the 32 x 32 x 32 instruction: 20 % of the products at D = 128
+// computed for nothing, 11 % now), and the short chains (three MFMAs at w = 11) with a 4-register accumulator keep
+// the kernel at 116 VGPRs, four waves per SIMD (round 5: 66.1 -> 55.2 us at config C SSD,
+// profiles/probes_r05/ab_ssd_16x16_r05.txt).  Per output row:
 //   * stage: the window's new row enters the R / L records (one byte per record), the row that left is zeroed;
 //   * SB: V(c) = Σ b'^2 of R column c's record (four v_dot4_i32_i8), an exclusive wave prefix X of V, then
 //     SB(m) = X(n + w) - X(n) for n = m - m_lo, and the key table -T(n), T(n) = (SB << 8) + 255 - n, in LDS;
-//   * B operands for both sub-tiles and every K-step; per m-block the A operands of its K-steps, the MFMAs of the
-//     sub-tiles it serves and the epilogue: -key = 512 C - T(n) (one v_lshl_add_u32 per product, the MFMA writing
-//     VGPRs: -amdgpu-mfma-vgpr-form), invalid d masked in the two edge blocks, a running max per sub-tile;
+//   * B operands for the four sub-tiles and every K-step; per m-block the A operands of its K-steps, the MFMAs of
+//     the sub-tiles it serves and the epilogue: -key = 512 C - T(n) (one v_lshl_add_u32 per product, the MFMA
+//     writing VGPRs: -amdgpu-mfma-vgpr-form), invalid d masked in the two edge blocks, a running max per sub-tile;
 //   * key = (SB - 2C) * 256 + 255 - n: the minimum is the smallest cost, ties -> the largest m = the smallest d
 //     (the SAD kernels' rule); |SB - 2C| * 256 < 2^31 for w <= 11.
-// The C/D layout is column = lane & 31 (x), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (m): the reduction over m
-// stays in the lane's registers; one half-wave swap at the end.  Integer arithmetic: bit-exact with the oracle.
+// The C/D layout is column = lane & 15 (x), row = 4 (lane >> 4) + r (m): the reduction over m runs over the
+// lane's four registers, then across the four lane groups (two swaps) at the end of the row.  Integer
+// arithmetic: bit-exact with the oracle.
 #include <algorithm>
 
 #include "usv_sad_common.hpp"
@@ -47,38 +53,37 @@ typedef int mi32x16 __attribute__((ext_vector_type(16)));
 template <int RAD, int DB>
 struct MCfg {
     static constexpr int WIN = 2 * RAD + 1;
-    static constexpr int NS = 2;              // 32-column sub-tiles per wave
-    static constexpr int XT = 32 * NS;        // output columns per wave
-    static constexpr int NBM = NS + DB;       // 32-row m-blocks
-    static constexpr int NM = 32 * NBM;       // R window centres per tile
-    static constexpr int NSTEP = RAD + 1;     // K-steps: window columns 2 s, 2 s + 1 (column w reads zeros)
-    static constexpr int NRC = 256;           // R records (columns rs .. rs + 255; NM + 16 are read)
-    static constexpr int NLC = 128;           // L records (XT + 16 are read)
+    static constexpr int NS = 4;              // 16-column sub-tiles per wave
+    static constexpr int XT = 16 * NS;        // output columns per wave
+    static constexpr int DB16 = 2 * DB;       // D / 16
+    static constexpr int NBM = NS + DB16;     // 16-row m-blocks
+    static constexpr int NM = 16 * NBM;       // R window centres per tile
+    static constexpr int NSTEP = (WIN + 3) / 4;  // K-steps: window columns 4 s .. 4 s + 3 (columns >= w read zeros)
+    static constexpr int NRC = 256;           // R records (columns rs .. rs + 255)
+    static constexpr int NLC = 128;           // L records
     static constexpr int R_OFF = 0;
     static constexpr int L_OFF = R_OFF + 16 * NRC;
     static constexpr int Z_OFF = L_OFF + 16 * NLC;       // one zero record
     static constexpr int X_OFF = Z_OFF + 16;             // exclusive prefix of V (256 i32)
     static constexpr int T_OFF = X_OFF + 4 * 256;        // key tables -T(n), two rows (2 x 256 i32)
     static constexpr int M_OFF = T_OFF + 8 * 256;        // window byte masks by first ring slot (16 x 16 B)
-    static constexpr int LUT_OFF = M_OFF + 16 * 16;      // distance table (256 f64)
-    static constexpr int SMEM = LUT_OFF + 8 * 256;
+    static constexpr int SMEM = M_OFF + 16 * 16;
     static_assert(WIN <= 11, "|SB - 2C| * 256 fits an i32 key for w <= 11");
     static_assert(NM <= 256, "key low byte: 255 - n");
-    static_assert(NM + 16 <= NRC && XT + 16 <= NLC && NRC == 256 && NLC == 128, "records: 4 / 2 per lane");
-    static_assert(WIN <= 15, "the window's rows and the one leaving fit the 16-slot ring");
+    static_assert(NM + 4 * NSTEP <= NRC && XT + 4 * NSTEP <= NLC && NRC == 256 && NLC == 128, "records: 4 / 2 per lane");
 };
 
 #ifndef USV_SSD_MFMA_OCC
-#define USV_SSD_MFMA_OCC 3  // waves per SIMD the kernel is compiled for
+#define USV_SSD_MFMA_OCC 4  // waves per SIMD the kernel is compiled for
 #endif
 template <int RAD, int DB>
 __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
                                                       uint8_t* __restrict__ disp, double* __restrict__ dist,
                                                       MatchArgs a, int n_xt, int bands) {
     using C = MCfg<RAD, DB>;
-    constexpr int WIN = C::WIN, NS = C::NS, XT = C::XT, NBM = C::NBM, NSTEP = C::NSTEP, D = 32 * DB;
+    constexpr int WIN = C::WIN, NS = C::NS, XT = C::XT, NBM = C::NBM, NSTEP = C::NSTEP, DB16 = C::DB16, D = 32 * DB;
     __shared__ __attribute__((aligned(16))) uint8_t smem[C::SMEM];
-    const int l = threadIdx.x, j = l & 31, h = l >> 5;
+    const int l = threadIdx.x, j = l & 15, g = l >> 4;
     int blk = blockIdx.x;
     const int xt = blk % n_xt;
     blk /= n_xt;
@@ -98,9 +103,10 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
     const __amdgpu_buffer_rsrc_t rsrcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(R), (short)0, 0x7FFFFFFF, 0x00020000);
 
-    // every record starts empty (zero); the zero record; the window masks; the distance table
+    // every record starts empty (zero); the zero record; the window masks (the distance table is read from
+    // global memory: 2 KB less LDS per workgroup lets four one-wave workgroups per SIMD fit)
     for (int i = l; i < (C::X_OFF) / 16; i += 64) reinterpret_cast<mi32x4*>(smem)[i] = mi32x4{0, 0, 0, 0};
-    if (l < 64) {  // mask f: bytes of ring slots f .. f + w - 1 (mod 16)
+    {  // mask f: bytes of ring slots f .. f + w - 1 (mod 16)
         const int f = l >> 2, q = l & 3;
         uint32_t m = 0;
 #pragma unroll
@@ -108,8 +114,6 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
             if (((4 * q + e - f) & 15) < WIN) m |= 0xFFu << (8 * e);
         reinterpret_cast<uint32_t*>(smem + C::M_OFF)[l] = m;
     }
-    if (dist)
-        for (int i = l; i < 256; i += 64) reinterpret_cast<double*>(smem + C::LUT_OFF)[i] = a.lut[i];
 
     // a row's staged bytes, lane l: R columns rs + l + 64 q (q < 4; records l + 64 q), L columns ls + l + 64 q
     // (q < 2), clamped to the image (replicate border).  Strided records keep the byte stores of one instruction
@@ -196,15 +200,14 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
     uint32_t pr[4], pl[2];  // loaded one row ahead: R row y + 1 + r, L row y + r
     load_r(y_begin + 1 + RAD, pr);
     load_l(y_begin + RAD, pl);
-    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
     const mi32x4* recR = reinterpret_cast<const mi32x4*>(smem + C::R_OFF);
     const mi32x4* recL = reinterpret_cast<const mi32x4*>(smem + C::L_OFF);
 
-    // the edge blocks' valid-d lane masks, one per accumulator register r (C row (r & 3) + 8 (r >> 2) + 4 h against
-    // column j), computed once: loop-invariant lane masks the selects below read from SGPRs
-    bool below[16];
+    // the edge blocks' valid-d lane masks, one per accumulator register r (C row 4 g + r against column j),
+    // computed once: loop-invariant lane masks the selects below read from SGPRs
+    bool below[4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) below[r] = j < (r & 3) + 8 * (r >> 2) + 4 * h;
+    for (int r = 0; r < 4; ++r) below[r] = j < 4 * g + r;
     for (int y = y_begin; y < y_end; ++y) {
         // L: row y + r enters the window, row y - r - 1 left; R: row y + 1 + r for the next row's table
         if (y > y_begin) put_l(y - RAD - 1, kClearL);
@@ -216,63 +219,57 @@ __global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const ui
             load_l(y + 1 + RAD, pl);
             make_table(y + 1);  // independent of this row's MFMAs: the compiler interleaves the two
         }
-        // B operands (L records): sub-tile t, K-step s -> window column dx = 2 s + h of output column x0 + 32 t + j
+        // B operands: sub-tile t, K-step s -> window column dx = 4 s + g of output column x0 + 16 t + j
         mi32x4 Bop[NS][NSTEP];
 #pragma unroll
         for (int s = 0; s < NSTEP; ++s) {
-            const int dx = 2 * s + h;
+            const int dx = 4 * s + g;
 #pragma unroll
             for (int t = 0; t < NS; ++t)
-                Bop[t][s] = dx < WIN ? recL[32 * t + j + dx] : *reinterpret_cast<const mi32x4*>(smem + C::Z_OFF);
+                Bop[t][s] = dx < WIN ? recL[16 * t + j + dx] : *reinterpret_cast<const mi32x4*>(smem + C::Z_OFF);
         }
         int run[NS];  // running max of -key
 #pragma unroll
         for (int t = 0; t < NS; ++t) run[t] = (int)0x80000000u;
+        const int* Tt = reinterpret_cast<const int*>(smem + C::T_OFF + 1024 * (y & 1));
 #pragma unroll
         for (int b = 0; b < NBM; ++b) {
             mi32x4 Aop[NSTEP];
 #pragma unroll
-            for (int s = 0; s < NSTEP; ++s) Aop[s] = recR[32 * b + j + 2 * s + h];
-            const mi32x4* Tb = reinterpret_cast<const mi32x4*>(smem + C::T_OFF + 1024 * (y & 1) + 4 * (32 * b + 4 * h));
-            mi32x4 Tv[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) Tv[g] = Tb[2 * g];  // rows 8 g + 4 h .. + 3 of the block
-            // (each sub-tile's MFMA chain right before its epilogue: both chains first, so the matrix pipe runs
-            // one while the VALU reduces the other, needs two live accumulators -- 242 VGPRs or spills, slower)
+            for (int s = 0; s < NSTEP; ++s) Aop[s] = recR[16 * b + j + 4 * s + g];
+            const mi32x4 Tv = *reinterpret_cast<const mi32x4*>(Tt + 16 * b + 4 * g);  // rows 4 g .. 4 g + 3
 #pragma unroll
             for (int t = 0; t < NS; ++t) {
-                if (b < t || b > t + DB) continue;
-                mi32x16 acc = {};
+                if (b < t || b > t + DB16) continue;
+                mi32x4 acc = {0, 0, 0, 0};
 #pragma unroll
-                for (int s = 0; s < NSTEP; ++s)
-                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aop[s], Bop[t][s], acc, 0, 0, 0);
-                int k[16];
+                for (int s = 0; s < NSTEP; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(Aop[s], Bop[t][s], acc, 0, 0, 0);
+                int k[4];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) k[r] = (acc[r] << 9) + Tv[r >> 2][r & 3];  // -key: one v_lshl_add_u32
+                for (int r = 0; r < 4; ++r) k[r] = (acc[r] << 9) + Tv[r];
                 if (b == t) {  // d = D + j - i: valid for j < i
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) k[r] = below[r] ? k[r] : (int)0x80000000u;
-                } else if (b == t + DB) {  // d = j - i: valid for j >= i
+                    for (int r = 0; r < 4; ++r) k[r] = below[r] ? k[r] : (int)0x80000000u;
+                } else if (b == t + DB16) {  // d = j - i: valid for j >= i
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) k[r] = below[r] ? (int)0x80000000u : k[r];
+                    for (int r = 0; r < 4; ++r) k[r] = below[r] ? (int)0x80000000u : k[r];
                 }
-                int m = run[t];
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) m = max(max(m, k[r]), k[r + 1]);
-                run[t] = m;
+                run[t] = max(max(run[t], k[0]), max(max(k[1], k[2]), k[3]));
             }
         }
-        // a column's rows are split over the two half-waves: combine; lane (j, h) writes sub-tile h's column j
+        // a column's rows are spread over the four 16-lane groups: combine; lane (j, g) writes sub-tile g's column j
 #pragma unroll
-        for (int t = 0; t < NS; ++t) run[t] = max(run[t], __shfl_xor(run[t], 32, 64));
-        // (every select in this kernel is compiler-visible C++, not sel_mask()'s inline asm: the compiler pads the
-        // MFMA wait states of its own instructions only, and an asm select placed in an MFMA's shadow by the
-        // scheduler wrote an operand register the MFMA was still reading -- tests/test_isa_lint.py checks)
-        const int key = -(h ? run[1] : run[0]);
-        const int d = 32 * h + j + D - 255 + (key & 0xFF);
-        const int x = x0 + 32 * h + j;
+        for (int t = 0; t < NS; ++t) {
+            run[t] = max(run[t], __shfl_xor(run[t], 16, 64));
+            run[t] = max(run[t], __shfl_xor(run[t], 32, 64));
+        }
+        // (every select in this kernel is compiler-visible C++, not inline asm: the compiler pads the MFMA wait
+        // states of its own instructions only -- tests/test_isa_lint.py checks)
+        const int key = -(g == 0 ? run[0] : g == 1 ? run[1] : g == 2 ? run[2] : run[3]);
+        const int d = 16 * g + j + D - 255 + (key & 0xFF);
+        const int x = x0 + 16 * g + j;
         disp[(size_t)y * a.disp_pitch + x] = (uint8_t)d;
-        if (dist) dist[(size_t)y * a.dist_pitch + x] = lut_s[d];
+        if (dist) dist[(size_t)y * a.dist_pitch + x] = a.lut[d];
     }
 }
 
