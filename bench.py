@@ -796,7 +796,8 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), steps * 8, s, preload="self")
     out["ssd_matrix"] = {"workload": f"{W}x{H} w={w} D={D} SSD", "us": us, "value": W * H / (us * 1e-6),
                          "kernel": "ssd_mfma_kernel (v_mfma_i32_16x16x64_i8)",
-                         "mfma_tops": 2.0 * 32 * 32 * 32 * (60 * H * ((W + 63) // 64)) / (us * 1e-6) / 1e12}
+                         "mfma_tops": 2.0 * 16 * 16 * 64 * (4 * (D // 16 + 1) * ((w + 3) // 4) * H * ((W + 63) // 64))
+                         / (us * 1e-6) / 1e12}
     for kernel, n in (("tiled", steps * 8), ("generic", steps)):
         ssd = StereoBlockMatcher(D, w, "ssd", kernel=kernel)
         us = time_launches(lambda: ssd.compute(Lt, Rt, out_disp=d1), n, s, preload="self")
@@ -808,8 +809,9 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
     out["note"] = "AUTO runs ssd_matrix for SSD at w <= 11 and D = 32..160 step 32, ssd_fast at 11 <= w <= 15 " \
                   "otherwise, and the tiled kernel (vertical running sums, LDS-DMA row ring) for other SSD windows " \
                   "and for shapes outside the fast kernels (W % 4, W < 48, unaligned pitch or base); generic = one " \
-                  "thread per pixel, direct window, only for w > 31; mfma_tops counts the 60 MFMAs per 64-column " \
-                  "tile-row the matrix kernel issues at D = 128 (padding included)"
+                  "thread per pixel, direct window, only for w > 31; mfma_tops counts the MFMAs the matrix kernel " \
+                  "issues (4 sub-tiles x (D/16 + 1) m-blocks x ceil(w/4) K-steps of 16x16x64 per 64-column tile-row: " \
+                  "108 at D = 128, w = 11; edge triangles and the zero window column included)"
     return out
 
 
