@@ -68,6 +68,35 @@ def test_batch_sharded_config_d_host_buffers(gpu):
 
 
 @pytest.mark.gpu
+def test_batch_sharded_pitched_host_buffers(gpu):
+    """Host frames with a row pitch > W and a pair stride > pitch * H take the per-frame 2-D copies; a dense batch
+    takes one copy per camera and shard: both give the same maps."""
+    import torch
+    n = torch.cuda.device_count()
+    W, H, D, w, B, pitch = 256, 96, 64, 7, 3, 272
+    pairs = [synthetic_pair(W, H, D, pair_index=90 + i, noise=2) for i in range(B)]
+    stride = pitch * H + 64
+    Lp = np.zeros(stride * B, dtype=np.uint8)
+    Rp = np.zeros(stride * B, dtype=np.uint8)
+    for i, (l, r, _) in enumerate(pairs):
+        Lp[i * stride:i * stride + pitch * H].reshape(H, pitch)[:, :W] = l
+        Rp[i * stride:i * stride + pitch * H].reshape(H, pitch)[:, :W] = r
+    eng = ShardedMatcher(list(range(n)), B, W, H, D, w)
+    try:
+        dense, _ = eng.run(np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs]))
+        disp = np.zeros((B, H, W), dtype=np.uint8)
+        vp = ctypes.c_void_p
+        _lib.check("usv_batch_sharded", eng.lib.usv_batch_sharded(
+            eng.handle, vp(Lp.ctypes.data), vp(Rp.ctypes.data), B, stride, pitch, vp(disp.ctypes.data), None, None,
+            0))
+        assert np.array_equal(disp, dense)
+        for i, (l, r, _) in enumerate(pairs):
+            assert np.array_equal(disp[i], oracle_sad(l, r, D, w, "sad", "sliding", threads=16)), i
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_batch_sharded_resident_inputs(gpu):
     """Frames already in HBM (usv_sharded_input_buffers), results read from the root's gather buffer."""
     import torch

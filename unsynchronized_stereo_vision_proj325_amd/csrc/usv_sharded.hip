@@ -149,14 +149,24 @@ usv_status submit(usv_sharded_engine* e, const uint8_t* L, const uint8_t* R, int
         hipStream_t hs = s.stream[k];
         if (count == 0) return;
         if (host_in) {
-            for (int b = 0; b < count; ++b) {
-                const size_t src = (size_t)(first + b) * pair_stride;
-                if (hipMemcpy2DAsync(s.L[k] + b * frame, e->W, L + src, pitch, e->W, e->H, hipMemcpyHostToDevice,
-                                     hs) != hipSuccess ||
-                    hipMemcpy2DAsync(s.R[k] + b * frame, e->W, R + src, pitch, e->W, e->H, hipMemcpyHostToDevice,
-                                     hs) != hipSuccess) {
+            if ((size_t)pitch == (size_t)e->W && pair_stride == frame) {
+                // a dense batch: the shard's frames are one run per camera, one copy each
+                const size_t src = (size_t)first * frame, n = (size_t)count * frame;
+                if (hipMemcpyAsync(s.L[k], L + src, n, hipMemcpyHostToDevice, hs) != hipSuccess ||
+                    hipMemcpyAsync(s.R[k], R + src, n, hipMemcpyHostToDevice, hs) != hipSuccess) {
                     st[k] = USV_ERR_HIP;
                     return;
+                }
+            } else {
+                for (int b = 0; b < count; ++b) {
+                    const size_t src = (size_t)(first + b) * pair_stride;
+                    if (hipMemcpy2DAsync(s.L[k] + b * frame, e->W, L + src, pitch, e->W, e->H,
+                                         hipMemcpyHostToDevice, hs) != hipSuccess ||
+                        hipMemcpy2DAsync(s.R[k] + b * frame, e->W, R + src, pitch, e->W, e->H,
+                                         hipMemcpyHostToDevice, hs) != hipSuccess) {
+                        st[k] = USV_ERR_HIP;
+                        return;
+                    }
                 }
             }
             if (hipEventRecord(s.h2d[k], hs) != hipSuccess) {

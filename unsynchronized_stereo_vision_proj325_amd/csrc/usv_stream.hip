@@ -30,9 +30,9 @@ struct usv_frame_stream {
     int W = 0, H = 0, D = 0, w = 0, metric = 0, depth = 0, flags = 0, device = 0;
     size_t frame = 0;  // W * H
     struct Slot {
-        uint8_t *hL = nullptr, *hR = nullptr, *hDisp = nullptr;  // pinned host staging
+        uint8_t *hL = nullptr, *hR = nullptr, *hDisp = nullptr;  // pinned host staging (hR = hL + frame)
         double* hDist = nullptr;                                 // pinned (USV_STREAM_DEVICE_DIST)
-        uint8_t *dL = nullptr, *dR = nullptr, *dDisp = nullptr;  // device
+        uint8_t *dL = nullptr, *dR = nullptr, *dDisp = nullptr;  // device (dR = dL + frame)
         double* dDist = nullptr;
         hipEvent_t in = nullptr, matched = nullptr, done = nullptr;  // after the H2D, the match, the D2H
         long long ticket = -1;  // frame in this slot, -1 = free
@@ -53,12 +53,10 @@ usv::HostPool& host_pool() {
 }
 
 void free_slot(usv_frame_stream::Slot& s) {
-    (void)hipHostFree(s.hL);
-    (void)hipHostFree(s.hR);
+    (void)hipHostFree(s.hL);  // hR = hL + frame
     (void)hipHostFree(s.hDisp);
     (void)hipHostFree(s.hDist);
-    (void)hipFree(s.dL);
-    (void)hipFree(s.dR);
+    (void)hipFree(s.dL);  // dR = dL + frame
     (void)hipFree(s.dDisp);
     (void)hipFree(s.dDist);
     if (s.in) (void)hipEventDestroy(s.in);
@@ -117,11 +115,11 @@ usv_status usv_frame_stream_create(int W, int H, int D, int w, int metric, int d
     e->slot.resize((size_t)depth);
     const bool dd = flags & USV_STREAM_DEVICE_DIST;
     for (auto& s : e->slot) {
-        if (hipHostMalloc(&s.hL, e->frame, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(&s.hR, e->frame, hipHostMallocDefault) != hipSuccess ||
+        // L and R back to back in one pinned and one device allocation: the pair crosses the link as ONE copy
+        // (round 5: depth 3 0.106 -> 0.097 ms per 1080p frame, profiles/probes_r05/ab_stream_contig_r05.txt)
+        if (hipHostMalloc(&s.hL, 2 * e->frame, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc(&s.hDisp, e->frame, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(&s.dL, e->frame) != hipSuccess || hipMalloc(&s.dR, e->frame) != hipSuccess ||
-            hipMalloc(&s.dDisp, e->frame) != hipSuccess ||
+            hipMalloc(&s.dL, 2 * e->frame) != hipSuccess || hipMalloc(&s.dDisp, e->frame) != hipSuccess ||
             (dd && (hipHostMalloc(&s.hDist, e->frame * sizeof(double), hipHostMallocDefault) != hipSuccess ||
                     hipMalloc(&s.dDist, e->frame * sizeof(double)) != hipSuccess)) ||
             hipEventCreateWithFlags(&s.in, hipEventDisableTiming) != hipSuccess ||
@@ -130,6 +128,8 @@ usv_status usv_frame_stream_create(int W, int H, int D, int w, int metric, int d
             release(e);
             return USV_ERR_HIP;
         }
+        s.hR = s.hL + e->frame;
+        s.dR = s.dL + e->frame;
     }
     if (hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_match, hipStreamNonBlocking) != hipSuccess ||
@@ -187,8 +187,7 @@ usv_status usv_frame_stream_submit(usv_frame_stream* e, const uint8_t* L, const 
         for (hipStream_t q : {e->s_in, e->s_match, e->s_out}) (void)hipStreamSynchronize(q);
         return st;
     };
-    if (hipMemcpyAsync(s.dL, s.hL, e->frame, hipMemcpyHostToDevice, e->s_in) != hipSuccess ||
-        hipMemcpyAsync(s.dR, s.hR, e->frame, hipMemcpyHostToDevice, e->s_in) != hipSuccess ||
+    if (hipMemcpyAsync(s.dL, s.hL, 2 * e->frame, hipMemcpyHostToDevice, e->s_in) != hipSuccess ||
         hipEventRecord(s.in, e->s_in) != hipSuccess || hipStreamWaitEvent(e->s_match, s.in, 0) != hipSuccess)
         return drain(USV_ERR_HIP);
     const bool dd = e->flags & USV_STREAM_DEVICE_DIST;
