@@ -806,7 +806,7 @@ def fallback_legs(dev, L: np.ndarray, R: np.ndarray, D: int, w: int, steps: int)
         us = time_launches(lambda: sad.compute(Lc, Rc, out_disp=d2), n, s, preload="self")
         out[f"sad_{kernel}_w1918"] = {"workload": f"1918x{H} (pitch {W}) w={w} D={D} SAD", "us": us,
                                       "value": 1918 * H / (us * 1e-6)}
-    out["note"] = "AUTO runs ssd_matrix for SSD at w <= 11 and D = 32..160 step 32, ssd_fast at 11 <= w <= 15 " \
+    out["note"] = "AUTO runs ssd_matrix for SSD at w <= 13 and D = 32..160 step 32, ssd_fast at 11 <= w <= 15 " \
                   "otherwise, and the tiled kernel (vertical running sums, LDS-DMA row ring) for other SSD windows " \
                   "and for shapes outside the fast kernels (W % 4, W < 48, unaligned pitch or base); generic = one " \
                   "thread per pixel, direct window, only for w > 31; mfma_tops counts the MFMAs the matrix kernel " \

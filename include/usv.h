@@ -90,8 +90,8 @@ typedef enum {
                                W % 4 == 0, W >= 48, 4-byte aligned bases / pitch; UNSUPPORTED otherwise */
     USV_KERNEL_GENERIC = 2, /* direct-window kernel, any w <= 63, SAD or SSD (reference-speed fallback) */
     USV_KERNEL_TILED = 3,   /* sliding-window kernel: SAD or SSD, any W / pitch / alignment, w <= 31 */
-    USV_KERNEL_MATRIX = 4   /* SSD whose window cross term runs on the matrix cores (v_mfma_i32_32x32x32_i8):
-                               w = 3 .. 11, D = 32 .. 160 in steps of 32, W >= 64; USV_KERNEL_AUTO takes it for
+    USV_KERNEL_MATRIX = 4   /* SSD whose window cross term runs on the matrix cores (v_mfma_i32_16x16x64_i8):
+                               w = 3 .. 13, D = 32 .. 160 in steps of 32, W >= 64; USV_KERNEL_AUTO takes it for
                                every SSD shape it supports */
 } usv_kernel;
 

@@ -43,9 +43,10 @@ def test_matrix_ssd_config_c_full_size(gpu):
 
 
 @pytest.mark.parametrize("W,H,D,w", [(64, 16, 32, 3), (65, 20, 64, 5), (200, 77, 96, 7), (333, 41, 128, 9),
-                                     (1000, 50, 160, 11), (128, 300, 128, 11), (96, 9, 32, 11), (130, 33, 160, 3)])
+                                     (1000, 50, 160, 11), (128, 300, 128, 11), (96, 9, 32, 11), (130, 33, 160, 3),
+                                     (200, 45, 128, 13), (64, 14, 160, 13)])
 def test_matrix_ssd_shapes(gpu, W, H, D, w):
-    """Every window 3..11 and D = 32..160: border tiles (the first m-blocks left of column 0, the last tile shifted
+    """Every window 3..13 and D = 32..160: border tiles (the first m-blocks left of column 0, the last tile shifted
     to W - 64 and overlapping its neighbour), bands of a few rows, frames barely one tile wide."""
     rng = np.random.default_rng(W * 31 + H * 7 + D + w)
     L = rng.integers(0, 256, (H, W), dtype=np.uint8)
@@ -55,7 +56,7 @@ def test_matrix_ssd_shapes(gpu, W, H, D, w):
     assert np.array_equal(got, ref), (W, H, D, w, _mismatch(got, ref))
 
 
-@pytest.mark.parametrize("w", [3, 5, 7, 9, 11])
+@pytest.mark.parametrize("w", [3, 5, 7, 9, 11, 13])
 @pytest.mark.parametrize("D", [32, 64, 96, 128, 160])
 def test_matrix_ssd_every_instantiation(gpu, w, D):
     """Every (w, D) the kernel is instantiated for (ssd_mfma_kernel<(w - 1) / 2, D / 32>), each compiled
@@ -81,9 +82,10 @@ def test_matrix_ssd_ties(gpu, levels):
     assert np.array_equal(got, ref), _mismatch(got, ref)
 
 
-def test_matrix_ssd_extreme_costs(gpu):
-    """0 against 255 (the largest SSD, 121 x 255^2): the i32 keys must not wrap; all-tie and constant images."""
-    H, W, D, w = 40, 192, 96, 11
+@pytest.mark.parametrize("w", [11, 13])
+def test_matrix_ssd_extreme_costs(gpu, w):
+    """0 against 255 (the largest SSD, w^2 x 255^2): the i32 keys must not wrap; all-tie and constant images."""
+    H, W, D = 40, 192, 96
     L = np.zeros((H, W), dtype=np.uint8)
     R = np.full((H, W), 255, dtype=np.uint8)
     R[:, ::7] = 0
@@ -118,9 +120,9 @@ def test_matrix_ssd_pitched_unaligned_and_batched(gpu):
         assert np.array_equal(out[i], ref), (i, _mismatch(out[i], ref))
 
 
-@pytest.mark.parametrize("W,H,D,w", [(128, 16, 100, 11), (128, 16, 192, 11), (128, 16, 64, 13), (60, 16, 32, 5)])
+@pytest.mark.parametrize("W,H,D,w", [(128, 16, 100, 11), (128, 16, 192, 11), (128, 16, 64, 15), (60, 16, 32, 5)])
 def test_matrix_ssd_refuses_unsupported(gpu, W, H, D, w):
-    """Outside w <= 11, D in 32..160 step 32, W >= 64 the selector refuses (AUTO falls back to the VALU kernels)."""
+    """Outside w <= 13, D in 32..160 step 32, W >= 64 the selector refuses (AUTO falls back to the VALU kernels)."""
     L = torch.zeros((H, W), dtype=torch.uint8, device=gpu)
     with pytest.raises(_lib.UsvError):
         StereoBlockMatcher(D, w, "ssd", kernel="matrix").compute(L, L)

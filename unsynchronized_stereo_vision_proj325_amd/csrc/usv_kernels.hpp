@@ -58,7 +58,7 @@ hipError_t launch_pair(const MatchArgs& a, hipStream_t s);
 // SSD kernel (usv_sad_ssd.hip): 11 <= w <= 15, on shapes fast_path_supported accepts.
 hipError_t launch_ssd(const MatchArgs& a, hipStream_t s);
 
-// SSD with the window cross term on the matrix cores (usv_ssd_mfma.hip): w = 3 .. 11, D = 32 .. 192 in steps of
+// SSD with the window cross term on the matrix cores (usv_ssd_mfma.hip): w = 3 .. 13, D = 32 .. 160 in steps of
 // 32, W >= 64, any pitch / alignment.  hipErrorInvalidValue otherwise.
 bool ssd_mfma_supported(const MatchArgs& a);
 hipError_t launch_ssd_mfma(const MatchArgs& a, hipStream_t s);

@@ -1,5 +1,5 @@
 // usv_ssd_mfma.hip -- SSD block match with the window's cross term on the gfx950 matrix cores
-// (ssd_mfma_kernel: v_mfma_i32_16x16x64_i8; w <= 11, D a multiple of 32 up to 160).
+// (ssd_mfma_kernel: v_mfma_i32_16x16x64_i8; w <= 13, D a multiple of 32 up to 160).
 //
 // Spec: SURVEY.md §8(a) A1, SSD variant (restated in oracle/sad_oracle.c).  With a' = a - 128 and b' = b - 128
 // (signed bytes, exact: a' = (int8)(a ^ 0x80)), for output pixel x, disparity d and R window centre m = x - d:
@@ -36,7 +36,8 @@
 //     the sub-tiles it serves and the epilogue: -key = 512 C - T(n) (one v_lshl_add_u32 per product, the MFMA
 //     writing VGPRs: -amdgpu-mfma-vgpr-form), invalid d masked in the two edge blocks, a running max per sub-tile;
 //   * key = (SB - 2C) * 256 + 255 - n: the minimum is the smallest cost, ties -> the largest m = the smallest d
-//     (the SAD kernels' rule); |SB - 2C| * 256 < 2^31 for w <= 11.
+//     (the SAD kernels' rule).  Range: per pixel b'^2 - 2 a'b' lies in [-128^2, 128^2 + 2 * 128 * 127 = 48896], so
+//     |(SB - 2C) * 256 + 255| < 2^31 and 512 C - T(n) stays inside an i32 for w <= 13 (169 * 48896 * 256 < 2^31).
 // The C/D layout is column = lane & 15 (x), row = 4 (lane >> 4) + r (m): the reduction over m runs over the
 // lane's four registers, then across the four lane groups (two swaps) at the end of the row.  Integer
 // arithmetic: bit-exact with the oracle.
@@ -68,16 +69,17 @@ struct MCfg {
     static constexpr int T_OFF = X_OFF + 4 * 256;        // key tables -T(n), two rows (2 x 256 i32)
     static constexpr int M_OFF = T_OFF + 8 * 256;        // window byte masks by first ring slot (16 x 16 B)
     static constexpr int SMEM = M_OFF + 16 * 16;
-    static_assert(WIN <= 11, "|SB - 2C| * 256 fits an i32 key for w <= 11");
+    static_assert(WIN <= 13, "|SB - 2C| * 256 fits an i32 key for w <= 13");
     static_assert(NM <= 256, "key low byte: 255 - n");
     static_assert(NM + 4 * NSTEP <= NRC && XT + 4 * NSTEP <= NLC && NRC == 256 && NLC == 128, "records: 4 / 2 per lane");
 };
 
 #ifndef USV_SSD_MFMA_OCC
-#define USV_SSD_MFMA_OCC 4  // waves per SIMD the kernel is compiled for
+#define USV_SSD_MFMA_OCC 4  // waves per SIMD the kernel is compiled for (w = 13: 3, its four-step B operands need
+                            // 64 VGPRs and would spill at 128)
 #endif
 template <int RAD, int DB>
-__global__ __launch_bounds__(64, USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
+__global__ __launch_bounds__(64, RAD >= 6 ? 3 : USV_SSD_MFMA_OCC) void ssd_mfma_kernel(const uint8_t* __restrict__ Lg, const uint8_t* __restrict__ Rg,
                                                       uint8_t* __restrict__ disp, double* __restrict__ dist,
                                                       MatchArgs a, int n_xt, int bands) {
     using C = MCfg<RAD, DB>;
@@ -308,8 +310,8 @@ hipError_t launch_mfma_r(const MatchArgs& a, hipStream_t s) {
 }  // namespace
 
 bool ssd_mfma_supported(const MatchArgs& a) {
-    // SSD, w = 3 .. 11, D = 32 .. 160 in steps of 32, at least one 64-column tile, 32-bit row offsets
-    return a.metric == 1 && (a.w & 1) && a.w >= 3 && a.w <= 11 && a.D % 32 == 0 && a.D >= 32 && a.D <= 160 &&
+    // SSD, w = 3 .. 13, D = 32 .. 160 in steps of 32, at least one 64-column tile, 32-bit row offsets
+    return a.metric == 1 && (a.w & 1) && a.w >= 3 && a.w <= 13 && a.D % 32 == 0 && a.D >= 32 && a.D <= 160 &&
            a.W >= 64 && (long long)a.pitch * a.H < (1LL << 31);
 }
 
@@ -321,6 +323,7 @@ hipError_t launch_ssd_mfma(const MatchArgs& a, hipStream_t s) {
         case 3: return launch_mfma_r<3>(a, s);
         case 4: return launch_mfma_r<4>(a, s);
         case 5: return launch_mfma_r<5>(a, s);
+        case 6: return launch_mfma_r<6>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
