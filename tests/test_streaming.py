@@ -33,6 +33,51 @@ def test_expand_distance_host_matches_table():
         assert np.array_equal(got[~np.isinf(got)], exp[~np.isinf(exp)])
 
 
+def test_expand_distance_after_fork_and_from_threads():
+    """The host expansion's persistent workers (csrc/usv_host_pool.hpp): a forked child that calls it after the
+    parent has started its workers completes (it gets its own pool instead of waiting on threads it does not
+    have), a call asking for far more threads than the host has is capped, and two callers at once both finish
+    with the right maps (the second runs on its own threads instead of queueing behind the first)."""
+    import os
+    import threading
+    import time
+    lut = _ref_lut()
+    rng = np.random.default_rng(9)
+    disp = rng.integers(1, 256, (300, 97), dtype=np.uint8)
+    exp = lut[disp]
+    assert np.array_equal(expand_distance(disp, lut, threads=8), exp)  # parent's workers now exist
+    assert np.array_equal(expand_distance(disp, lut, threads=100000), exp)  # capped, one part per row at most
+    pid = os.fork()
+    if pid == 0:  # child: any failure or exception is a non-zero exit status
+        code = 1
+        try:
+            ok = all(np.array_equal(expand_distance(disp, lut, threads=t), exp) for t in (4, 16, 4))
+            code = 0 if ok else 2
+        finally:
+            os._exit(code)
+    deadline = time.monotonic() + 60
+    while True:
+        wpid, status = os.waitpid(pid, os.WNOHANG)
+        if wpid:
+            break
+        if time.monotonic() > deadline:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            pytest.fail("forked child hung in usv_distance_expand_host")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+    results = [None] * 4
+
+    def worker(i):
+        results[i] = all(np.array_equal(expand_distance(disp, lut, threads=6), exp) for _ in range(20))
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert results == [True] * 4
+
+
 def test_expand_distance_pitched_output():
     lut = _ref_lut()
     disp = np.arange(64 * 10, dtype=np.uint32).astype(np.uint8).reshape(10, 64)[:, :50]

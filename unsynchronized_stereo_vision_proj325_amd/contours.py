@@ -118,8 +118,8 @@ _MATCHERS: dict[int, ContourMatcherGPU] = {}
 _MATCHERS_LOCK = __import__("threading").Lock()
 # The matcher holds max_contours^2 x 16 B of pinned host memory and twice that on the device (score rows and
 # the compacted list): the per-device cache keeps one of at most _CACHE_MAX_CONTOURS contours (4096: 268 MB
-# pinned); larger sets get a matcher for the call only, and sets above the C matcher's limit take the
-# descriptor + score launches with the selection done by torch on the device.
+# pinned); larger sets take the descriptor + score launches with the selection done by torch on the device
+# (n^2 x 8 B of scores instead of a per-call matcher's n^2 x 48 B of pinned host and device buffers).
 _CACHE_MAX_CONTOURS = 4096
 _MATCHER_MAX_CONTOURS = 16384  # usv_contour_matcher_create's limit
 
@@ -146,16 +146,12 @@ def GenerateMatchingListGPU(contours_l, contours_r, device="cuda", stream=None):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     n = max(len(contours_l), len(contours_r))
     p = max(sum(len(c) for c in contours_l), sum(len(c) for c in contours_r))
-    if n > _MATCHER_MAX_CONTOURS:
+    if n > _CACHE_MAX_CONTOURS:
+        # a matcher for one call would pin n^2 x 16 B on the host and twice that on the device (4.3 GB and
+        # 8.6 GB at n = 16384), allocated and freed per call; the descriptor + score launches with the
+        # selection on the device need only the n^2 x 8 B score matrix
         with torch.cuda.device(idx):
             return _select_on_device(contours_l, contours_r, torch.device("cuda", idx))
-    if n > _CACHE_MAX_CONTOURS:
-        with torch.cuda.device(idx):
-            m = ContourMatcherGPU(n, max(1 << 16, p))
-        try:
-            return m(contours_l, contours_r)
-        finally:
-            m.close()
     with _MATCHERS_LOCK:
         m = _MATCHERS.get(idx)
         if m is None or not m.fits(n, n, p, p):

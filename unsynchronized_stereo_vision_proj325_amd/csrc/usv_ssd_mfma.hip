@@ -116,6 +116,9 @@ __global__ __launch_bounds__(64, RAD >= 6 ? 3 : USV_SSD_MFMA_OCC) void ssd_mfma_
             if (((4 * q + e - f) & 15) < WIN) m |= 0xFFu << (8 * e);
         reinterpret_cast<uint32_t*>(smem + C::M_OFF)[l] = m;
     }
+    // LDS hand-offs between lanes of the one wave: its LDS operations execute in program order, and a
+    // wave_barrier (no instruction) keeps the compiler from moving a read of another lane's store above it
+    __builtin_amdgcn_wave_barrier();
 
     // a row's staged bytes, lane l: R columns rs + l + 64 q (q < 4; records l + 64 q), L columns ls + l + 64 q
     // (q < 2), clamped to the image (replicate border).  Strided records keep the byte stores of one instruction
@@ -173,6 +176,7 @@ __global__ __launch_bounds__(64, RAD >= 6 ? 3 : USV_SSD_MFMA_OCC) void ssd_mfma_
         incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
         const int ex = incl - tot;
         reinterpret_cast<mi32x4*>(smem + C::X_OFF)[l] = mi32x4{ex, ex + v[0], ex + p1, ex + p2};
+        __builtin_amdgcn_wave_barrier();  // X is read at other lanes' offsets
         const int* X = reinterpret_cast<const int*>(smem + C::X_OFF);
         int* T = reinterpret_cast<int*>(smem + C::T_OFF + 1024 * (yy & 1));
         int xa[(C::NM + 63) / 64], xb[(C::NM + 63) / 64];
@@ -198,6 +202,7 @@ __global__ __launch_bounds__(64, RAD >= 6 ? 3 : USV_SSD_MFMA_OCC) void ssd_mfma_
             put_l(rho, vl);
         }
     }
+    __builtin_amdgcn_wave_barrier();
     make_table(y_begin);
     uint32_t pr[4], pl[2];  // loaded one row ahead: R row y + 1 + r, L row y + r
     load_r(y_begin + 1 + RAD, pr);
@@ -211,12 +216,15 @@ __global__ __launch_bounds__(64, RAD >= 6 ? 3 : USV_SSD_MFMA_OCC) void ssd_mfma_
 #pragma unroll
     for (int r = 0; r < 4; ++r) below[r] = j < 4 * g + r;
     for (int y = y_begin; y < y_end; ++y) {
+        // (the previous row's record and table reads stay above this row's record stores)
+        __builtin_amdgcn_wave_barrier();
         // L: row y + r enters the window, row y - r - 1 left; R: row y + 1 + r for the next row's table
         if (y > y_begin) put_l(y - RAD - 1, kClearL);
         put_l(y + RAD, pl);
         const bool more = y + 1 < y_end;
+        if (more) put_r(y + 1 + RAD, pr);
+        __builtin_amdgcn_wave_barrier();  // the records are read at other lanes' offsets below
         if (more) {
-            put_r(y + 1 + RAD, pr);
             load_r(y + 2 + RAD, pr);
             load_l(y + 1 + RAD, pl);
             make_table(y + 1);  // independent of this row's MFMAs: the compiler interleaves the two

@@ -18,6 +18,7 @@
 // for it (usv_distance_expand_host), so the link carries 1 B per pixel instead
 // of 9.  USV_STREAM_DEVICE_DIST keeps the f64 map on the device path as well.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <functional>
 #include <vector>
@@ -46,10 +47,17 @@ struct usv_frame_stream {
 
 namespace {
 
-// the expansion's workers (usv_host_pool.hpp); never destroyed, so no worker is joined during static destruction
+// the expansion's workers (usv_host_pool.hpp); never destroyed, so no worker is joined during static destruction.
+// One pool per process: a forked child finds its parent's pool (whose threads it does not have) and installs a
+// fresh one; the parent's copy is left untouched (a HostPool never locks or joins in a process it was not made in).
 usv::HostPool& host_pool() {
-    static usv::HostPool* pool = new usv::HostPool;
-    return *pool;
+    static std::atomic<usv::HostPool*> pool{nullptr};
+    usv::HostPool* p = pool.load(std::memory_order_acquire);
+    if (p && p->owner() == getpid()) return *p;
+    auto* fresh = new usv::HostPool;
+    if (pool.compare_exchange_strong(p, fresh, std::memory_order_acq_rel)) return *fresh;
+    delete fresh;  // another thread of this process installed one first (p now holds it); fresh has no workers
+    return *p;
 }
 
 void free_slot(usv_frame_stream::Slot& s) {

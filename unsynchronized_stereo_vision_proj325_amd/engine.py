@@ -172,6 +172,10 @@ class StereoBlockMatcher:
         pointer argument, so a caller stepping a frame stream from Python pays the launch itself instead of
         compute()'s per-call validation and argument marshalling.  The buffers must stay alive (and
         unmoved) while the callable is used; the plan is freed with the callable.
+
+        The callable always launches on the stream that was current (or passed as `stream`) when bind() ran,
+        also when it is called inside another ``torch.cuda.stream(...)`` context -- unlike compute(), which
+        follows the current stream on every call.  The callable holds that stream object alive with its buffers.
         """
         import weakref
 
@@ -180,7 +184,8 @@ class StereoBlockMatcher:
                      stream=stream)  # validation + one real launch (raises exactly as compute() does)
         lib = _lib.load()
         with torch.cuda.device(left.device):
-            s = _stream(stream)
+            stream_obj = torch.cuda.current_stream() if stream is None else stream
+            s = stream_obj.cuda_stream
             lut = self.lut_device(left.device) if with_distance else None
             batched = left.dim() == 3
             H, W = left.shape[-2], left.shape[-1]
@@ -193,7 +198,7 @@ class StereoBlockMatcher:
                 out_dist.stride(0) if (with_distance and batched) else 0,
                 out_dist.stride(-2) if with_distance else 0, lut.data_ptr() if with_distance else None,
                 _KERNELS[self.kernel] if not batched else _lib.KERNEL_AUTO, s, ctypes.byref(plan)))
-        keep = (left, right, out_disp, out_dist, lut)  # the callable holds its buffers alive
+        keep = (left, right, out_disp, out_dist, lut, stream_obj)  # the callable holds its buffers and stream alive
         fn, handle, check = lib.usv_match_plan_launch, plan.value, _lib.check
 
         def launch():
