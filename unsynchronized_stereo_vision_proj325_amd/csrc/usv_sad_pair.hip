@@ -71,7 +71,11 @@ struct PCfg {
     // writes and one combine buffer suffices (slot addresses are then compile-time); two or more waves
     // alternate two buffers so a flush needs one barrier
     static constexpr int NCB = NW == 1 ? 1 : 2;
-    static constexpr int LUT_OFF = COMB_OFF + NCB * KRB * NW * K;
+    // comb row stride (words): NW x K, padded to 24 at two waves.  The flush reads a row per lane (16-byte reads,
+    // 16-lane groups) and a row's quarter per lane (8-byte reads, 32-lane groups); at a 16-word stride both put
+    // rows r and r + 4 on the same banks, at 24 every row of a group lands on its own banks.
+    static constexpr int CSTR = NW == 1 ? K : NW * K + 8;
+    static constexpr int LUT_OFF = COMB_OFF + NCB * KRB * CSTR;
     // distance table in LDS: one wave means D <= 128, so every output disparity is < 128 and half the
     // table suffices (1 KB less: the static ring's 12 workgroups per CU fit only below ~12.5 KB each,
     // profiles/probes_r04/lds_residency_r04.txt)
@@ -395,14 +399,14 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         asm volatile("" : "+v"(tid));
         if (wide) {
             static_assert(K == 8, "one 8-byte disparity store per row");
-            const uint32_t* crow = comb + (C::NCB > 1 ? cb * KRB * NW * K : 0);
+            const uint32_t* crow = comb + (C::NCB > 1 ? cb * KRB * C::CSTR : 0);
             if (tid < rows) {
-                uint4 k0 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[0];
-                uint4 k1 = reinterpret_cast<const uint4*>(crow + tid * NW * K)[1];
+                uint4 k0 = reinterpret_cast<const uint4*>(crow + tid * C::CSTR)[0];
+                uint4 k1 = reinterpret_cast<const uint4*>(crow + tid * C::CSTR)[1];
 #pragma unroll
                 for (int w2 = 1; w2 < NW; ++w2) {
-                    const uint4 m0 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[0];
-                    const uint4 m1 = reinterpret_cast<const uint4*>(crow + (tid * NW + w2) * K)[1];
+                    const uint4 m0 = reinterpret_cast<const uint4*>(crow + tid * C::CSTR + w2 * K)[0];
+                    const uint4 m1 = reinterpret_cast<const uint4*>(crow + tid * C::CSTR + w2 * K)[1];
                     k0 = make_uint4(min(k0.x, m0.x), min(k0.y, m0.y), min(k0.z, m0.z), min(k0.w, m0.w));
                     k1 = make_uint4(min(k1.x, m1.x), min(k1.y, m1.y), min(k1.z, m1.z), min(k1.w, m1.w));
                 }
@@ -415,10 +419,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             if (dist && tid < 4 * rows) {
                 struct __attribute__((aligned(8))) D2 { double a, b; };
                 const int r = tid >> 2, q = tid & 3;
-                uint2 kk = reinterpret_cast<const uint2*>(crow + r * NW * K)[q];
+                uint2 kk = reinterpret_cast<const uint2*>(crow + r * C::CSTR)[q];
 #pragma unroll
                 for (int w2 = 1; w2 < NW; ++w2) {
-                    const uint2 m = reinterpret_cast<const uint2*>(crow + (r * NW + w2) * K)[q];
+                    const uint2 m = reinterpret_cast<const uint2*>(crow + r * C::CSTR + w2 * K)[q];
                     kk = make_uint2(min(kk.x, m.x), min(kk.y, m.y));
                 }
                 const size_t y = (size_t)(y_chunk + r);
@@ -433,7 +437,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             const int row = i / K, p = i - row * K;
             uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
-            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[(((C::NCB > 1 ? cb : 0) * KRB + row) * NW + w2) * K + p]);
+            for (int w2 = 0; w2 < NW; ++w2) key = min(key, comb[((C::NCB > 1 ? cb : 0) * KRB + row) * C::CSTR + w2 * K + p]);
             const uint32_t dv = key & 0xFFu;
             const size_t y = (size_t)(y_chunk + row);
             disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
@@ -527,7 +531,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 asm volatile("" : "+v"(px));
                 px = (px & 63) >> 3;
             }
-            comb[(((C::NCB > 1 ? cb : 0) * KRB + slot) * NW + wave) * K + px] = fm;
+            comb[((C::NCB > 1 ? cb : 0) * KRB + slot) * C::CSTR + wave * K + px] = fm;
         }
     };
     auto tr_finish = [&](int slot) {
@@ -608,6 +612,421 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
     const int rest = nout % KRB;
     if (rest) flush(rest);
     wait_vmcnt<0>();
+}
+
+// ===================================================================================
+// K = 16 form of the paired kernel (r = 5, D <= 128: config C), two waves per SIMD.
+//
+// Same lane mapping as above (lane = disparities d, d + 1 of one 128-disparity wave), 16 output columns per
+// x-tile instead of 8.  Per 16 columns and row: the prefix chain has 26 steps (52 v_sad; all 27 prefix positions
+// are read, since K > w leaves no run to jump), the row sums, running sums and ring 3 x 16, the argmin
+// 32 keys per lane.  Against two K = 8 tiles: 52 instead of 2 x 34 chain VALU, 14 instead of 2 x 10 entry
+// reads, 3 instead of 2 x 3 row DMAs and 26 instead of 2 x 18 L-byte extractions for the same outputs; the
+// argmin and the H / S work per column are unchanged.  The price is the ring: 11 rows x 16 columns of
+// (d, d + 1) pairs = 176 VGPRs, so the kernel is compiled for two waves per SIMD (256 VGPRs) instead of three,
+// and a band covers 1 / 8 instead of 1 / 12 of a CU's rows (more warm-up rows per output row).
+// ===================================================================================
+#ifndef USV_PAIR_K16
+#define USV_PAIR_K16 0  // 1: config C's shape (r = 5, D <= 128) takes sad_pair16_kernel
+#endif
+#ifndef USV_PAIR16_RA
+#define USV_PAIR16_RA 0  // > 0: this many entry pairs of row t + 1 are read before row t's argmin
+#endif
+#ifndef USV_PAIR16_GEN_WEIGHTS
+#define USV_PAIR16_GEN_WEIGHTS 0x3C3C3C64u  // band heights by dispatch generation: 100 : 60 (two generations)
+#endif
+
+struct P16 {
+    static constexpr int RAD = 5, K = 16, WIN = 2 * RAD + 1;
+    static constexpr int NPOS = K + 2 * RAD;         // 26 chain steps
+    static constexpr int NV = (NPOS + 2) / 2;         // 14 ds_read_b64: entries 0 .. 26 (+ one unused)
+    static constexpr int NR = 2 * 63 + 2 * NV;        // entries a wave stages per row
+    static constexpr int NQ = (NR + 63) / 64;         // DMA instructions per row
+    static constexpr int NRS = NQ * 64;
+    static constexpr int NB = WIN, PD = NB - 1;       // static ring: row t in slot t mod WIN
+    static constexpr int KRB = WIN;                   // output rows per flush
+    // transpose buffer: pixel x's 64 words at 68 x (see pair16_band_loop); 16 pixels
+    static constexpr int TSTR = 68;
+    static constexpr int TB_OFF = NB * NRS;
+    static constexpr int COMB_OFF = TB_OFF + K * TSTR;  // per-row minima, KRB rows x 16 pixels
+    static constexpr int LUT_OFF = COMB_OFF + KRB * K;
+    static constexpr int LUTN = 128;                  // one wave: every disparity < 128
+    static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN;
+    static constexpr int RA = USV_PAIR16_RA;
+    static_assert(NQ == 3 && PD * NQ < 64, "three DMAs per row; look-ahead fits the 6-bit vmcnt");
+    static_assert(TB_OFF % 4 == 0 && COMB_OFF % 4 == 0 && LUT_OFF % 4 == 0, "16-byte aligned regions");
+    static_assert(NV <= 15 && RA >= 0 && RA < NV, "counted lgkmcnt waits hold at most 15 reads");
+};
+
+template <int EDGE>
+__device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                                 uint8_t* __restrict__ disp, double* __restrict__ dist,
+                                                 const MatchArgs& a, uint32_t* smem, int lane, int x0, int y_begin,
+                                                 int y_end) {
+    using C = P16;
+    constexpr int RAD = C::RAD, WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, NPOS = C::NPOS, NV = C::NV;
+    constexpr int KRB = C::KRB, RA = C::RA;
+    using LS = LSeg<RAD, EDGE, K>;
+    using LWords = typename SWords<LS::NLD>::T;
+    const int lmax = min(63, a.D / 2 - 1);
+    const int l_eff = min(lane, lmax);
+    const int cbase = x0 - RAD - (2 * 63 + 1);  // first R column the wave stages
+    uint32_t* rbuf = smem;
+    uint32_t* comb = smem + C::COMB_OFF;
+    uint32_t* tb = smem + C::TB_OFF;
+    // Transpose: lane l stores word x (pixel x's (d, d + 1) costs) at tb[68 x + l]; lane m = 4p + q reads pixel p's
+    // words of source lanes 16 q .. 16 q + 15 as four 16-byte windows j = 0..3 at 68 p + 16 q + 4 j.  Window j of
+    // lane (p, q) starts on bank slot (p + 4 q + j) mod 16 (4-bank slots), and each 16-lane read group of a
+    // ds_read_b128 is four q times four values of p mod 4, so every group reads 16 distinct slots: conflict-free
+    // with the windows in fixed order -- one address VGPR, the window in the instruction's offset.
+    // dlo[j]: the four source lanes' d = 2 (16 q + 4 j + e) as bytes (lanes past lmax replay lane lmax's costs with a
+    // larger d, so their keys never win).
+    const int p_lane = lane >> 2, q_lane = lane & 3;
+    const uint32_t tr_addr = lds_addr(tb) + 4u * (uint32_t)(C::TSTR * p_lane + 16 * q_lane);
+    uint32_t dlo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dlo[j] = (uint32_t)(32 * q_lane + 8 * j) * 0x01010101u + 0x06040200u;
+    const double* lut_s = reinterpret_cast<const double*>(smem + C::LUT_OFF);
+    const int s_l = 2 * (63 - l_eff);  // this lane's first staged entry
+    const int nout = y_end - y_begin;
+    const int T = nout + 2 * RAD;
+    const int Hm1 = a.H - 1, Wm1 = a.W - 1;
+    auto row_off = [&](int t) -> uint32_t {
+        const int y = min(max(y_begin - RAD + t, 0), Hm1);
+        return (uint32_t)(y * a.pitch);
+    };
+    const uint8_t* const Lseg = L + LS::base(x0);
+    const uint8_t* const Rdma = R - kDmaBias;
+    const int y0 = y_begin - RAD;
+    const int last_off = Hm1 * a.pitch;
+    int rawL = (y0 + WIN + 1) * a.pitch, rawR = (y0 + WIN + PD) * a.pitch;
+    const su4 rsrc = [&] {
+        const uint64_t base = reinterpret_cast<uint64_t>(Rdma);
+        su4 r;
+        r[0] = (uint32_t)base;
+        r[1] = (uint32_t)(base >> 32);
+        r[2] = 0xFFFFFFFFu;
+        r[3] = 0x00020000u;
+        return r;
+    }();
+    uint32_t colRb[C::NQ];
+#pragma unroll
+    for (int i = 0; i < C::NQ; ++i)
+        colRb[i] = (uint32_t)min(max(cbase + lane + 64 * i, 0), Wm1) + kDmaBias - 256u * (uint32_t)i;
+    const uint32_t rbase = lds_addr(rbuf);
+    auto issue_dma = [&](int t, int buf) {
+        dma_row<C::NQ>(Rdma + row_off(t), colRb, rbase + 4u * (uint32_t)(buf * C::NRS));
+    };
+    LWords lw_next;
+    auto load_lw = [&](int t) { lw_next = s_load_words_pin<LS::NLD>(Lseg, row_off(t)); };
+    const uint32_t ra0 = lds_addr(rbuf + s_l);
+    // the entries as single ds_read_b64 (inline asm: the compiler would pair them into ds_read2_b64), pairs [k0, k1)
+    // of ring slot I, each retired by a counted lgkmcnt wait before the first chain step that needs it (in-order LDS
+    // returns)
+    u2x ev[NV];
+    auto issue_reads = [&](auto i_tag, auto k0t, auto k1t) {
+        constexpr int I = decltype(i_tag)::value, k0 = decltype(k0t)::value, k1 = decltype(k1t)::value;
+        constexpr uint32_t BOFF = 4u * (uint32_t)(I * C::NRS);
+        [&]<int... Kk>(std::integer_sequence<int, Kk...>) {
+            (ds_read_b64_at<BOFF + 8u * (k0 + Kk)>(ev[k0 + Kk], ra0), ...);
+        }(std::make_integer_sequence<int, k1 - k0>{});
+    };
+
+    // One input row t (ring slot I = t mod WIN): R DMA of row t + PD, the entry reads (pairs [RA, NV) when the first RA
+    // were read ahead: those are retired by the L words' lgkmcnt(0)), the 26-step chain with the row sums
+    // H[x] = A[x + WIN] - A[x] folded into the running sums as soon as A[x + WIN] exists.
+    auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K]) {
+        constexpr bool WARM = decltype(warm_tag)::value;
+        constexpr int I = decltype(i_tag)::value;
+        constexpr int K0 = WARM ? 0 : RA;  // pairs read ahead
+        int t = t_in;
+        asm volatile("" : "+s"(t));
+        wait_vmcnt<(PD - 1) * C::NQ>();
+        __builtin_amdgcn_wave_barrier();
+        constexpr int SLOT_NEXT = (I + PD) % NB;
+        if constexpr (WARM) {
+            issue_dma(t + PD, SLOT_NEXT);
+        } else {
+            int rr = rawR;
+            asm volatile("" : "+s"(rr));
+            dma_row3_at_min<4u * SLOT_NEXT * C::NRS>(rsrc, rr, last_off, colRb, rbase);
+            rawR = rr + a.pitch;
+        }
+        // the ring row leaving the window first: its registers are free for this row's entries
+        if constexpr (!WARM) {
+#pragma unroll
+            for (int x = 0; x < K; ++x) S[x] -= ring[I][x];
+        }
+        uint32_t Lv[NPOS];
+        {
+            uint32_t Lw[8];
+            wait_lgkm0_pin<LS::NLD>(lw_next);
+            LWords cur = lw_next;
+            unpack_words<LS::NLD>(cur, Lw);
+#pragma unroll
+            for (int j = 0; j < NPOS; ++j) {
+                const int bidx = LS::byte(j);
+                if (kLWholeWord<RAD, EDGE> && (bidx & 3) == 0) Lv[j] = Lw[bidx >> 2];
+                else Lv[j] = (Lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
+            }
+        }
+        issue_reads(i_tag, std::integral_constant<int, K0>{}, std::integral_constant<int, NV>{});
+        uint32_t E[2 * NV];
+        uint32_t A[NPOS + 1];
+        A[0] = 0;
+        auto chain_step = [&](auto jt) {
+            constexpr int j = decltype(jt)::value;
+            constexpr int kp = j == 0 ? -1 : j / 2;  // pairs [0, kp] retired by earlier steps
+            constexpr int kn = (j + 1) / 2;          // step j reads E[j], E[j + 1]
+            if constexpr (kn > kp) {
+                if constexpr (kn >= K0) {
+                    constexpr int later = NV - 1 - kn;
+                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_s_waitcnt(0xC07F | (later << 8));
+                    // both registers of a pair stay allocated up to the wait (the last pair's second entry is never
+                    // read)
+#pragma unroll
+                    for (int k = kp + 1; k <= kn; ++k) asm volatile("" ::"v"(ev[k]));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int k = kp + 1; k <= kn; ++k) {
+                    E[2 * k] = ev[k].x;
+                    E[2 * k + 1] = ev[k].y;
+                }
+            }
+            const uint32_t l = Lv[j];
+            A[j + 1] = __builtin_amdgcn_sad_hi_u8(l, E[j], __builtin_amdgcn_sad_u8(l, E[j + 1], A[j]));
+            if constexpr (j + 1 >= WIN) {
+                constexpr int x = j + 1 - WIN;
+                const uint32_t h = A[j + 1] - A[x];  // both halves in [0, 65535], no borrow
+                S[x] = S[x] + h;
+                ring[I][x] = h;
+            }
+        };
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (chain_step(std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, NPOS>{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (WARM) {
+            load_lw(t + 1);
+        } else {
+            int rl = rawL;
+            asm volatile("" : "+s"(rl));
+            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+            rawL = rl + a.pitch;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    int y_chunk = y_begin;
+    const bool wide = ((reinterpret_cast<uintptr_t>(disp + x0) | (uintptr_t)a.disp_pitch) & 3u) == 0;
+    // a chunk's outputs: lane r stores row r's 16 disparity bytes (one 16-byte store), lane 4r + q the row's
+    // distances 4q .. 4q + 3 (two 16-byte stores)
+    auto flush = [&](int rows) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops run in order
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        if (wide) {
+            if (tid < rows) {
+                const uint4* c4 = reinterpret_cast<const uint4*>(comb + tid * K);
+                uint32_t o[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 k = c4[i];  // byte 0 of each key is its disparity
+                    o[i] = __builtin_amdgcn_perm(k.y, k.x, 0x0c0c0400u) | __builtin_amdgcn_perm(k.w, k.z, 0x04000c0cu);
+                }
+                const size_t y = (size_t)(y_chunk + tid);
+                *reinterpret_cast<uint4*>(disp + y * a.disp_pitch + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            if (dist && tid < 4 * rows) {
+                struct __attribute__((aligned(8))) D2 { double a, b; };
+                const int r = tid >> 2, q = tid & 3;
+                const uint4 k = reinterpret_cast<const uint4*>(comb + r * K)[q];
+                double* o = dist + (size_t)(y_chunk + r) * a.dist_pitch + x0 + 4 * q;
+                *reinterpret_cast<D2*>(o) = D2{lut_s[k.x & 0xFFu], lut_s[k.y & 0xFFu]};
+                *reinterpret_cast<D2*>(o + 2) = D2{lut_s[k.z & 0xFFu], lut_s[k.w & 0xFFu]};
+            }
+            y_chunk += rows;
+            return;
+        }
+        const int items = rows * K;
+        for (int i = tid; i < items; i += 64) {
+            const int row = i / K, p = i - row * K;
+            const uint32_t dv = comb[row * K + p] & 0xFFu;
+            const size_t y = (size_t)(y_chunk + row);
+            disp[y * a.disp_pitch + x0 + p] = (uint8_t)dv;
+            if (dist) dist[y * a.dist_pitch + x0 + p] = lut_s[dv];
+        }
+        y_chunk += rows;
+    };
+    // Argmin of one row, whose window sums S are final: the 16 transpose stores (ds_write_addtid_b32: address
+    // M0 + offset + 4 lane) and the four transposed reads (inline asm, so the compiler has no load of its own to drain);
+    // with read-ahead, the first RA entry pairs of the next row (ring slot I_NEXT) are issued behind them and only
+    // the transpose is waited for (lgkmcnt(RA)); then per transposed word two keys (cost << 8) | d by v_perm folded
+    // into a v_min3 tree, two quad DPP rounds and the pixel's comb word.
+    const uint32_t tb_m0 = lds_addr(tb);
+    auto emit = [&](const uint32_t(&S)[K], int slot, auto inext_tag) {
+        constexpr int I_NEXT = decltype(inext_tag)::value;
+        asm volatile("s_mov_b32 m0, %16\n\ts_nop 0\n\t"
+                     "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:272\n\t"
+                     "ds_write_addtid_b32 %2 offset:544\n\tds_write_addtid_b32 %3 offset:816\n\t"
+                     "ds_write_addtid_b32 %4 offset:1088\n\tds_write_addtid_b32 %5 offset:1360\n\t"
+                     "ds_write_addtid_b32 %6 offset:1632\n\tds_write_addtid_b32 %7 offset:1904\n\t"
+                     "ds_write_addtid_b32 %8 offset:2176\n\tds_write_addtid_b32 %9 offset:2448\n\t"
+                     "ds_write_addtid_b32 %10 offset:2720\n\tds_write_addtid_b32 %11 offset:2992\n\t"
+                     "ds_write_addtid_b32 %12 offset:3264\n\tds_write_addtid_b32 %13 offset:3536\n\t"
+                     "ds_write_addtid_b32 %14 offset:3808\n\tds_write_addtid_b32 %15 offset:4080"
+                     :: "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(S[6]), "v"(S[7]),
+                        "v"(S[8]), "v"(S[9]), "v"(S[10]), "v"(S[11]), "v"(S[12]), "v"(S[13]), "v"(S[14]), "v"(S[15]),
+                        "s"(tb_m0) : "memory", "m0");
+        static_assert(4 * C::TSTR == 272, "the store offsets above are 4 x TSTR apart");
+        u4x trq[4];
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                     "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48"
+                     : "=&v"(trq[0]), "=&v"(trq[1]), "=&v"(trq[2]), "=&v"(trq[3]) : "v"(tr_addr) : "memory");
+        if constexpr (RA > 0 && I_NEXT >= 0) {
+            wait_vmcnt<(PD - 1) * C::NQ>();  // the next row's DMA has landed (issued PD - 1 rows ago)
+            issue_reads(std::integral_constant<int, I_NEXT>{}, std::integral_constant<int, 0>{},
+                        std::integral_constant<int, RA>{});
+            asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3])
+                         : "n"(RA) : "memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3]) : : "memory");
+        }
+        uint32_t fv[32];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t dl = dlo[j], dh = dlo[j] + 0x01010101u;  // d even: + 1 per byte, no carry
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t w = trq[j][e];
+                fv[8 * j + 2 * e] = __builtin_amdgcn_perm(w, dl, 0x0c050400u + (uint32_t)e);
+                fv[8 * j + 2 * e + 1] = __builtin_amdgcn_perm(w, dh, 0x0c070600u + (uint32_t)e);
+            }
+        }
+        uint32_t m[12];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) m[i] = min(min(fv[3 * i], fv[3 * i + 1]), fv[3 * i + 2]);
+        m[10] = fv[30];
+        m[11] = fv[31];
+        const uint32_t n0 = min(min(m[0], m[1]), m[2]), n1 = min(min(m[3], m[4]), m[5]);
+        const uint32_t n2 = min(min(m[6], m[7]), m[8]), n3 = min(min(m[9], m[10]), m[11]);
+        uint32_t fm = min(min(n0, n1), min(n2, n3));
+        fm = min(fm, dpp<kQuadSwap1>(fm));
+        fm = min(fm, dpp<kQuadSwap2>(fm));
+        comb[slot * K + p_lane] = fm;
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    uint32_t S[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) S[i] = 0;
+    uint32_t ring[WIN][K];
+    if (dist) lut_dma<C::LUTN / 128>(a.lut, smem + C::LUT_OFF, lane);
+    [&]<int... P>(std::integer_sequence<int, P...>) { (issue_dma(P, P % NB), ...); }(std::make_integer_sequence<int, PD>{});
+    load_lw(0);
+    using WarmT = std::integral_constant<bool, true>;
+    using SteadyT = std::integral_constant<bool, false>;
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
+    }(std::make_integer_sequence<int, WIN>{});
+    emit(S, 0, std::integral_constant<int, 0>{});  // output row 0; the first steady row (t = WIN) is in slot 0
+    // output row k = t - 2r sits in comb slot k mod KRB; the chunk leaves once slot KRB - 1 is written
+    auto step = [&](int t0, auto i_tag) {
+        constexpr int I = decltype(i_tag)::value;
+        do_row(t0 + I, SteadyT{}, i_tag, S, ring);
+        // (the band's last row reads ahead into a slot nobody uses: harmless, retired by the final lgkmcnt(0))
+        emit(S, (I + 1) % WIN, std::integral_constant<int, (I + 1) % NB>{});
+        if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+    };
+    int t0 = WIN;
+    if constexpr (EDGE == kInterior) {
+        for (; t0 + WIN <= T; t0 += WIN) {
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                (step(t0, std::integral_constant<int, I>{}), ...);
+            }(std::make_integer_sequence<int, WIN>{});
+        }
+    }
+    for (; t0 < T; t0 += WIN) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            bool go = true;
+            ((go = go && (t0 + I < T), go ? step(t0, std::integral_constant<int, I>{}) : void()), ...);
+        }(std::make_integer_sequence<int, WIN>{});
+    }
+    wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load (and any read-ahead) before the SGPRs are reused
+    const int rest = nout % KRB;
+    if (rest) flush(rest);
+    wait_vmcnt<0>();
+}
+
+__global__ __launch_bounds__(64, 2) void sad_pair16_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                                          uint8_t* __restrict__ disp, double* __restrict__ dist,
+                                                          MatchArgs a, BandPlan P, const uint2* __restrict__ tiles) {
+    __shared__ __attribute__((aligned(16))) uint32_t smem[P16::SMEM_WORDS];
+    const int lane = threadIdx.x & 63;
+    unsigned xtu, pair;
+    int y_begin, y_end;
+    if (tiles) {  // the launcher's table: x-tile | pair << 16, y_begin | y_end << 16
+        const uint2 t = tiles[blockIdx.x];
+        xtu = t.x & 0xFFFFu;
+        pair = t.x >> 16;
+        y_begin = (int)(t.y & 0xFFFFu);
+        y_end = (int)(t.y >> 16);
+    } else {
+        const TileSpan sp = tile_span(blockIdx.x, gridDim.x, P.n_xt, P.m, P.extra, P.gen_g, P.weights, a.H);
+        xtu = sp.xt;
+        pair = sp.pair;
+        y_begin = sp.y_begin;
+        y_end = sp.y_end;
+    }
+    constexpr int K = P16::K;
+    const int xt = (int)xtu;
+    const int n_xt = P.n_xt;
+    // interior tiles read L columns x0 - 8 .. x0 + 23: the one before the last stops at W - 2K
+    int x0 = xt * K;
+    if (xt == n_xt - 1) x0 = a.W - K;
+    else if (xt == n_xt - 2) x0 = min(x0, a.W - 2 * K);
+    L += (size_t)pair * a.pair_stride;
+    R += (size_t)pair * a.pair_stride;
+    disp += (size_t)pair * a.disp_stride;
+    if (dist) dist += (size_t)pair * a.dist_stride;
+    if (y_end <= y_begin) return;
+    if (xt == 0)
+        pair16_band_loop<kLeft>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+    else if (xt == n_xt - 1)
+        pair16_band_loop<kRight>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+    else
+        pair16_band_loop<kInterior>(L, R, disp, dist, a, smem, lane, x0, y_begin, y_end);
+}
+
+hipError_t launch_pair16(const MatchArgs& a, hipStream_t s) {
+    constexpr int K = P16::K, WIN = P16::WIN;
+    static const int per_cu = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, sad_pair16_kernel, 64, 0) != hipSuccess || v <= 0) v = 1;
+        return v;
+    }();
+    BandPlan P{};
+    P.n_xt = (a.W + K - 1) / K;
+    const long slots = (long)cu_count() * per_cu;
+    const long NC = (long)P.n_xt * a.batch;
+    long m = slots / NC;
+    if (m < 1) m = 1;
+    const long m_max = a.H / (kMinBandWins * WIN) > 0 ? a.H / (kMinBandWins * WIN) : 1;
+    if (m > m_max) m = m_max;
+    P.m = (int)m;
+    const long ex = slots - NC * m;
+    P.extra = (a.batch == 1 && ex > 0 && ex < P.n_xt && a.H / (m + 1) >= kMinBandWins * WIN) ? (int)ex : 0;
+    const long total = NC * m + P.extra;
+    if (total > 0x7FFFFFFFL) return hipErrorInvalidValue;
+    P.gen_g = (int)(4L * (cu_count() / 8));  // one generation = one workgroup per SIMD-wave slot
+    if (P.gen_g < 1) P.gen_g = 1;
+    const bool two = per_cu == 8 && total > 8L * P.gen_g;
+    P.weights = two ? USV_PAIR16_GEN_WEIGHTS : 0x01010101u;
+    const uint2* tiles = tile_table(1, 0x100 + 5 * 16 + 1, a, P.n_xt, P.m, P.extra, P.gen_g, P.weights, (unsigned)total, s);
+    hipLaunchKernelGGL(sad_pair16_kernel, dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a, P, tiles);
+    return hipGetLastError();
 }
 
 #ifndef USV_PAIR_OCC7
@@ -728,6 +1147,8 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
 bool pair_supported(const MatchArgs& a) { return a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15; }
 template <int RAD>
 hipError_t launch_pair_r(const MatchArgs& a, hipStream_t s) {
+    if constexpr (RAD == 5 && USV_PAIR_K16)
+        if (a.D <= 128) return launch_pair16(a, s);
     return a.D <= 128 ? launch_pair_rn<RAD, 1>(a, s) : launch_pair_rn<RAD, 2>(a, s);
 }
 
