@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU box (round 5): smoke, the whole -m gpu suite, the driver's bench command, a rocprofv3 kernel trace of it.
+# GPU box: smoke, the whole -m gpu suite, the driver's bench command, a rocprofv3 kernel trace of it.
 # Each GPU step has its own limit; the first failure ends the call.  TAG names gpurun_out/<TAG>.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r05full}; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-r06full}; mkdir -p $OUT
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
   echo "=== $name ($(date +%T))"

@@ -47,6 +47,9 @@ struct PCfg {
 #ifndef USV_PAIR_RDASM
 #define USV_PAIR_RDASM 1  // staged-entry reads as single ds_read_b64 (inline asm, explicit lgkmcnt waits): C 51.70 -> 49.32 us
 #endif
+#ifndef USV_PAIR_LEARLY
+#define USV_PAIR_LEARLY 5  // the next row's L segment is loaded before the row's chain (not after it) at r <= this
+#endif
 #ifndef USV_PAIR_M0REUSE
 #define USV_PAIR_M0REUSE 1  // static ring: transpose stores off the row DMA's M0; row clamp in the DMA's wait state (SALU -2.9 per row)
 #endif
@@ -219,6 +222,21 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 else Lv[j] = (Lw[bidx >> 2] >> (8 * (bidx & 3))) & 0xFFu;
             }
         }
+        // the next row's L segment: issued before the chain (r <= USV_PAIR_LEARLY: the whole chain covers its latency;
+        // an SMEM op in flight only makes the chain's counted LDS waits stricter) or after it.  Interleaved A/B
+        // (profiles/probes_r06/ab_k16_r06.txt): config C (r = 5) 43.90 -> 43.29 us per two-stream step, the one-launch
+        // kernel 48.27 -> 48.48 us; config E (r = 7) 495 -> 519 us, so r = 7 keeps the late load
+        constexpr bool LEARLY = RAD <= USV_PAIR_LEARLY;
+        auto next_lw = [&] {
+            if constexpr (WARM) {
+                load_lw(t + 1);
+            } else {
+                int rl = rawL;
+                asm volatile("" : "+s"(rl));
+                lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+                rawL = rl + a.pitch;
+            }
+        };
         auto lbyte = [&](int j) -> uint32_t { return Lv[j]; };
         // the 4 L bytes of quad increments j .. j + 3 as one dword (one funnel shift of two segment words when
         // the bytes are consecutive, i.e. interior tiles; the border tiles' replicated bytes are or-ed)
@@ -282,6 +300,8 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
                 for (int e = 0; e < C::VEC; ++e) E[k * C::VEC + e] = vget<C::VEC>(v, e);
             }
         }
+        // (after the pending transposed words' lgkmcnt(0) above, which would otherwise wait for it)
+        if constexpr (LEARLY) next_lw();
         // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half).  With the argmin
         // pipelined, piece j of the previous row's argmin follows chain step j and the pair is
         // fenced: the two independent dependency chains interleave instruction by instruction.
@@ -374,14 +394,7 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
             ring[I][x] = h;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (WARM) {
-            load_lw(t + 1);
-        } else {
-            int rl = rawL;
-            asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
-            rawL = rl + a.pitch;
-        }
+        if constexpr (!LEARLY) next_lw();
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -627,7 +640,11 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 // and a band covers 1 / 8 instead of 1 / 12 of a CU's rows (more warm-up rows per output row).
 // ===================================================================================
 #ifndef USV_PAIR_K16
-#define USV_PAIR_K16 0  // 1: config C's shape (r = 5, D <= 128) takes sad_pair16_kernel
+#define USV_PAIR_K16 0  // 1: config C's shape (r = 5, D <= 128) takes sad_pair16_kernel (variant builds only)
+#endif
+#if USV_PAIR_K16
+#ifndef USV_PAIR16_LEARLY
+#define USV_PAIR16_LEARLY 0  // 1: the next row's L segment is loaded before the row's chain
 #endif
 #ifndef USV_PAIR16_RA
 #define USV_PAIR16_RA 0  // > 0: this many entry pairs of row t + 1 are read before row t's argmin
@@ -771,6 +788,17 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             }
         }
         issue_reads(i_tag, std::integral_constant<int, K0>{}, std::integral_constant<int, NV>{});
+        auto next_lw = [&] {
+            if constexpr (WARM) {
+                load_lw(t + 1);
+            } else {
+                int rl = rawL;
+                asm volatile("" : "+s"(rl));
+                lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
+                rawL = rl + a.pitch;
+            }
+        };
+        if constexpr (USV_PAIR16_LEARLY) next_lw();  // (as in pair_band_loop: a loss here, 44.2 -> 44.8 us per step)
         uint32_t E[2 * NV];
         uint32_t A[NPOS + 1];
         A[0] = 0;
@@ -808,14 +836,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             (chain_step(std::integral_constant<int, J>{}), ...);
         }(std::make_integer_sequence<int, NPOS>{});
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (WARM) {
-            load_lw(t + 1);
-        } else {
-            int rl = rawL;
-            asm volatile("" : "+s"(rl));
-            lw_next = s_load_words_pin<LS::NLD>(Lseg, (uint32_t)min(rl, last_off));
-            rawL = rl + a.pitch;
-        }
+        if constexpr (!USV_PAIR16_LEARLY) next_lw();
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -1028,6 +1049,7 @@ hipError_t launch_pair16(const MatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(sad_pair16_kernel, dim3((unsigned)total), dim3(64), 0, s, a.L, a.R, a.disp, a.dist, a, P, tiles);
     return hipGetLastError();
 }
+#endif  // USV_PAIR_K16
 
 #ifndef USV_PAIR_OCC7
 #define USV_PAIR_OCC7 3  // waves per SIMD the r = 7 paired kernel is compiled for
@@ -1147,8 +1169,10 @@ hipError_t launch_pair_rn(const MatchArgs& a, hipStream_t s) {
 bool pair_supported(const MatchArgs& a) { return a.D > 64 && (a.D % 2) == 0 && a.w >= 11 && a.w <= 15; }
 template <int RAD>
 hipError_t launch_pair_r(const MatchArgs& a, hipStream_t s) {
-    if constexpr (RAD == 5 && USV_PAIR_K16)
+#if USV_PAIR_K16
+    if constexpr (RAD == 5)
         if (a.D <= 128) return launch_pair16(a, s);
+#endif
     return a.D <= 128 ? launch_pair_rn<RAD, 1>(a, s) : launch_pair_rn<RAD, 2>(a, s);
 }
 
