@@ -177,6 +177,10 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 
     u4x trq[2];  // the pipelined argmin's transposed words (tr_issue -> tr_piece)
     const uint32_t ra0 = lds_addr(rbuf + s_l);  // this lane's first staged entry in slot 0
+    // the staged-entry pairs of a row (single ds_read_b64 each, do_row).  (Reading the first 2 / 4 / 6 pairs of row
+    // t + 1 right after row t's transpose ties: 43.42 / 43.35 / 43.49 vs 43.39 us per step,
+    // profiles/probes_r06/ab_k16_r06.txt -- three waves per SIMD already cover that latency.)
+    u2x ev[C::NE_V / C::VEC];
     auto do_row = [&](int t_in, auto warm_tag, auto i_tag, uint32_t(&S)[K], uint32_t(&ring)[WIN][K], auto&& pre) {
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int I = decltype(i_tag)::value;
@@ -277,7 +281,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         // so the compiler has no pending read left to drain with a lgkmcnt(0) of its own.
         // (1: single-batch rows, r <= 6; 2: also r = 7's two batches, which spill 24 B at two waves)
         constexpr bool RDASM = C::VEC == 2 && (USV_PAIR_RDASM == 2 || (USV_PAIR_RDASM == 1 && C::SPLIT == 1));
-        u2x ev[NV];
         constexpr uint32_t BOFF = C::STATIC ? 4u * (uint32_t)(I * C::NRS) : 0u;
         uint32_t ra = ra0;
         if constexpr (RDASM && !C::STATIC) ra += 4u * (uint32_t)boff;
