@@ -154,7 +154,7 @@ struct usv_match_plan {
 
 extern "C" {
 
-const char* usv_version(void) { return "usv-mi355x 0.4.2 (gfx950, " USV_BUILD_KIND ")"; }
+const char* usv_version(void) { return "usv-mi355x 0.4.3 (gfx950, " USV_BUILD_KIND ")"; }
 
 usv_status usv_device_check(int* n_devices) {
     int n = 0;
