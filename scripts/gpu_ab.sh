@@ -10,7 +10,7 @@ P=${PTAG:-r06}   # profile tag: profiles/${P}_C, profiles/${P}_C16
 PT="python -u -m pytest -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread"
 for v in ${VT}; do
   echo "=== parity $v ($(date +%T))"
-  USV_LIB_PATH=$PWD/build_variants/$v.so timeout -k 10 600 $PT tests/test_gpu_parity.py > $OUT/vt_$v.log 2>&1 || { tail -5 $OUT/vt_$v.log; exit 1; }
+  USV_LIB_PATH=$PWD/${VARIANTS_DIR:-build_variants}/$v.so timeout -k 10 600 $PT tests/test_gpu_parity.py > $OUT/vt_$v.log 2>&1 || { tail -5 $OUT/vt_$v.log; exit 1; }
   tail -1 $OUT/vt_$v.log
 done
 if [ -z "$NO_AB" ]; then

@@ -655,6 +655,16 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
 #ifndef USV_PAIR16_GEN_WEIGHTS
 #define USV_PAIR16_GEN_WEIGHTS 0x3C3C3C64u  // band heights by dispatch generation: 100 : 60 (two generations)
 #endif
+#ifndef USV_PAIR16_MIDT
+#define USV_PAIR16_MIDT 0  // > 0: row t - 1's transposed words are read at chain step MIDT of row t, its argmin after the chain
+#endif
+
+// the four transposed reads of one argmin (inline asm: retired by the caller's explicit waits)
+__device__ __forceinline__ void ds_read_b128_x4(u4x (&q)[4], uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                 "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48"
+                 : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]) : "v"(addr) : "memory");
+}
 
 struct P16 {
     static constexpr int RAD = 5, K = 16, WIN = 2 * RAD + 1;
@@ -673,6 +683,9 @@ struct P16 {
     static constexpr int LUTN = 128;                  // one wave: every disparity < 128
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN;
     static constexpr int RA = USV_PAIR16_RA;
+    static constexpr int MIDT = USV_PAIR16_MIDT;
+    static_assert(MIDT == 0 || (RA == 0 && MIDT >= 2 * 4 && MIDT < NPOS), "mid-chain transpose: no read-ahead; "
+                  "the counted waits after step MIDT hold 4 more reads");
     static_assert(NQ == 3 && PD * NQ < 64, "three DMAs per row; look-ahead fits the 6-bit vmcnt");
     static_assert(TB_OFF % 4 == 0 && COMB_OFF % 4 == 0 && LUT_OFF % 4 == 0, "16-byte aligned regions");
     static_assert(NV <= 15 && RA >= 0 && RA < NV, "counted lgkmcnt waits hold at most 15 reads");
@@ -685,7 +698,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
                                                  int y_end) {
     using C = P16;
     constexpr int RAD = C::RAD, WIN = C::WIN, K = C::K, NB = C::NB, PD = C::PD, NPOS = C::NPOS, NV = C::NV;
-    constexpr int KRB = C::KRB, RA = C::RA;
+    constexpr int KRB = C::KRB, RA = C::RA, MIDT = C::MIDT;
     using LS = LSeg<RAD, EDGE, K>;
     using LWords = typename SWords<LS::NLD>::T;
     const int lmax = min(63, a.D / 2 - 1);
@@ -744,6 +757,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
     // of ring slot I, each retired by a counted lgkmcnt wait before the first chain step that needs it (in-order LDS
     // returns)
     u2x ev[NV];
+    u4x trq[4];  // MIDT: the pending output row's transposed words, in flight from chain step MIDT to the row's end
     auto issue_reads = [&](auto i_tag, auto k0t, auto k1t) {
         constexpr int I = decltype(i_tag)::value, k0 = decltype(k0t)::value, k1 = decltype(k1t)::value;
         constexpr uint32_t BOFF = 4u * (uint32_t)(I * C::NRS);
@@ -759,6 +773,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         constexpr bool WARM = decltype(warm_tag)::value;
         constexpr int I = decltype(i_tag)::value;
         constexpr int K0 = WARM ? 0 : RA;  // pairs read ahead
+        constexpr bool PEND = MIDT > 0 && !WARM;  // row t - 1's argmin is pending (its words are in the buffer)
         int t = t_in;
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * C::NQ>();
@@ -809,9 +824,17 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             constexpr int j = decltype(jt)::value;
             constexpr int kp = j == 0 ? -1 : j / 2;  // pairs [0, kp] retired by earlier steps
             constexpr int kn = (j + 1) / 2;          // step j reads E[j], E[j + 1]
+            constexpr bool TQ = PEND && j >= MIDT;   // the four transposed reads are the newest LDS operations
+            if constexpr (PEND && j == MIDT) {
+                // the entry registers of pairs < MIDT / 2 are dead: the transposed words take their place
+                __builtin_amdgcn_sched_barrier(0);
+                ds_read_b128_x4(trq, tr_addr);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if constexpr (kn > kp) {
                 if constexpr (kn >= K0) {
-                    constexpr int later = NV - 1 - kn;
+                    constexpr int later = NV - 1 - kn + (TQ ? 4 : 0);
+                    static_assert(later <= 15, "lgkmcnt holds 4 bits");
                     __builtin_amdgcn_sched_barrier(0);
                     __builtin_amdgcn_s_waitcnt(0xC07F | (later << 8));
                     // both registers of a pair stay allocated up to the wait (the last pair's second entry is never
@@ -838,7 +861,10 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         [&]<int... J>(std::integer_sequence<int, J...>) {
             (chain_step(std::integral_constant<int, J>{}), ...);
         }(std::make_integer_sequence<int, NPOS>{});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (PEND)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3]) : : "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!USV_PAIR16_LEARLY) next_lw();
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -890,8 +916,7 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
     // the transpose is waited for (lgkmcnt(RA)); then per transposed word two keys (cost << 8) | d by v_perm folded
     // into a v_min3 tree, two quad DPP rounds and the pixel's comb word.
     const uint32_t tb_m0 = lds_addr(tb);
-    auto emit = [&](const uint32_t(&S)[K], int slot, auto inext_tag) {
-        constexpr int I_NEXT = decltype(inext_tag)::value;
+    auto store_t = [&](const uint32_t(&S)[K]) {
         asm volatile("s_mov_b32 m0, %16\n\ts_nop 0\n\t"
                      "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %1 offset:272\n\t"
                      "ds_write_addtid_b32 %2 offset:544\n\tds_write_addtid_b32 %3 offset:816\n\t"
@@ -905,19 +930,8 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
                         "v"(S[8]), "v"(S[9]), "v"(S[10]), "v"(S[11]), "v"(S[12]), "v"(S[13]), "v"(S[14]), "v"(S[15]),
                         "s"(tb_m0) : "memory", "m0");
         static_assert(4 * C::TSTR == 272, "the store offsets above are 4 x TSTR apart");
-        u4x trq[4];
-        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-                     "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48"
-                     : "=&v"(trq[0]), "=&v"(trq[1]), "=&v"(trq[2]), "=&v"(trq[3]) : "v"(tr_addr) : "memory");
-        if constexpr (RA > 0 && I_NEXT >= 0) {
-            wait_vmcnt<(PD - 1) * C::NQ>();  // the next row's DMA has landed (issued PD - 1 rows ago)
-            issue_reads(std::integral_constant<int, I_NEXT>{}, std::integral_constant<int, 0>{},
-                        std::integral_constant<int, RA>{});
-            asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3])
-                         : "n"(RA) : "memory");
-        } else {
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3]) : : "memory");
-        }
+    };
+    auto argmin = [&](const u4x(&trq)[4], int slot) {
         uint32_t fv[32];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -940,6 +954,24 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         fm = min(fm, dpp<kQuadSwap1>(fm));
         fm = min(fm, dpp<kQuadSwap2>(fm));
         comb[slot * K + p_lane] = fm;
+    };
+    auto emit = [&](const uint32_t(&S)[K], int slot, auto inext_tag) {
+        constexpr int I_NEXT = decltype(inext_tag)::value;
+        store_t(S);
+        u4x trq[4];
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                     "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48"
+                     : "=&v"(trq[0]), "=&v"(trq[1]), "=&v"(trq[2]), "=&v"(trq[3]) : "v"(tr_addr) : "memory");
+        if constexpr (RA > 0 && I_NEXT >= 0) {
+            wait_vmcnt<(PD - 1) * C::NQ>();  // the next row's DMA has landed (issued PD - 1 rows ago)
+            issue_reads(std::integral_constant<int, I_NEXT>{}, std::integral_constant<int, 0>{},
+                        std::integral_constant<int, RA>{});
+            asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3])
+                         : "n"(RA) : "memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3]) : : "memory");
+        }
+        argmin(trq, slot);
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -955,14 +987,24 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
     [&]<int... I>(std::integer_sequence<int, I...>) {
         (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
     }(std::make_integer_sequence<int, WIN>{});
-    emit(S, 0, std::integral_constant<int, 0>{});  // output row 0; the first steady row (t = WIN) is in slot 0
+    // output row 0; the first steady row (t = WIN) is in slot 0
+    if constexpr (MIDT > 0) store_t(S);
+    else emit(S, 0, std::integral_constant<int, 0>{});
     // output row k = t - 2r sits in comb slot k mod KRB; the chunk leaves once slot KRB - 1 is written
     auto step = [&](int t0, auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
         do_row(t0 + I, SteadyT{}, i_tag, S, ring);
-        // (the band's last row reads ahead into a slot nobody uses: harmless, retired by the final lgkmcnt(0))
-        emit(S, (I + 1) % WIN, std::integral_constant<int, (I + 1) % NB>{});
-        if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+        if constexpr (MIDT > 0) {
+            // row t - 1's output k = t - 1 - 2r: slot I (its words are in registers: row t's may overwrite the buffer)
+            store_t(S);
+            argmin(trq, I);
+            if constexpr (I == KRB - 1) flush(KRB);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            // (the band's last row reads ahead into a slot nobody uses: harmless, retired by the final lgkmcnt(0))
+            emit(S, (I + 1) % WIN, std::integral_constant<int, (I + 1) % NB>{});
+            if constexpr ((I + 1) % WIN == KRB - 1) flush(KRB);
+        }
     };
     int t0 = WIN;
     if constexpr (EDGE == kInterior) {
@@ -979,8 +1021,16 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         }(std::make_integer_sequence<int, WIN>{});
     }
     wait_lgkm0_pin<LS::NLD>(lw_next);  // retire the unused last L load (and any read-ahead) before the SGPRs are reused
-    const int rest = nout % KRB;
-    if (rest) flush(rest);
+    if constexpr (MIDT > 0) {  // the last output row's argmin
+        ds_read_b128_x4(trq, tr_addr);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(trq[0]), "+v"(trq[1]), "+v"(trq[2]), "+v"(trq[3]) : : "memory");
+        argmin(trq, (nout - 1) % KRB);
+        const int rest = nout - (y_chunk - y_begin);
+        if (rest) flush(rest);
+    } else {
+        const int rest = nout % KRB;
+        if (rest) flush(rest);
+    }
     wait_vmcnt<0>();
 }
 
