@@ -684,8 +684,8 @@ struct P16 {
     static constexpr int SMEM_WORDS = LUT_OFF + 2 * LUTN;
     static constexpr int RA = USV_PAIR16_RA;
     static constexpr int MIDT = USV_PAIR16_MIDT;
-    static_assert(MIDT == 0 || (RA == 0 && MIDT >= 2 * 4 && MIDT < NPOS), "mid-chain transpose: no read-ahead; "
-                  "the counted waits after step MIDT hold 4 more reads");
+    static_assert(MIDT == 0 || (MIDT >= 2 * 4 && MIDT < NPOS && 2 * RA <= MIDT),
+                  "mid-chain transpose: the counted waits after step MIDT hold 4 more reads");
     static_assert(NQ == 3 && PD * NQ < 64, "three DMAs per row; look-ahead fits the 6-bit vmcnt");
     static_assert(TB_OFF % 4 == 0 && COMB_OFF % 4 == 0 && LUT_OFF % 4 == 0, "16-byte aligned regions");
     static_assert(NV <= 15 && RA >= 0 && RA < NV, "counted lgkmcnt waits hold at most 15 reads");
@@ -988,8 +988,15 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         (do_row(I, WarmT{}, std::integral_constant<int, I>{}, S, ring), ...);
     }(std::make_integer_sequence<int, WIN>{});
     // output row 0; the first steady row (t = WIN) is in slot 0
-    if constexpr (MIDT > 0) store_t(S);
-    else emit(S, 0, std::integral_constant<int, 0>{});
+    if constexpr (MIDT > 0) {
+        store_t(S);
+        if constexpr (RA > 0) {
+            wait_vmcnt<(PD - 1) * C::NQ>();
+            issue_reads(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, RA>{});
+        }
+    } else {
+        emit(S, 0, std::integral_constant<int, 0>{});
+    }
     // output row k = t - 2r sits in comb slot k mod KRB; the chunk leaves once slot KRB - 1 is written
     auto step = [&](int t0, auto i_tag) {
         constexpr int I = decltype(i_tag)::value;
@@ -997,6 +1004,11 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         if constexpr (MIDT > 0) {
             // row t - 1's output k = t - 1 - 2r: slot I (its words are in registers: row t's may overwrite the buffer)
             store_t(S);
+            if constexpr (RA > 0) {  // the next row's first RA entry pairs, covered by the argmin
+                wait_vmcnt<(PD - 1) * C::NQ>();
+                issue_reads(std::integral_constant<int, (I + 1) % NB>{}, std::integral_constant<int, 0>{},
+                            std::integral_constant<int, RA>{});
+            }
             argmin(trq, I);
             if constexpr (I == KRB - 1) flush(KRB);
             __builtin_amdgcn_sched_barrier(0);
