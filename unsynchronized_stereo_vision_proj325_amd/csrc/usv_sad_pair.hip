@@ -47,9 +47,6 @@ struct PCfg {
 #ifndef USV_PAIR_RDASM
 #define USV_PAIR_RDASM 1  // staged-entry reads as single ds_read_b64 (inline asm, explicit lgkmcnt waits): C 51.70 -> 49.32 us
 #endif
-#ifndef USV_PAIR_PRIO
-#define USV_PAIR_PRIO 0  // 1: a steady row raises its wave's issue priority from the row start until its loads are out
-#endif
 #ifndef USV_PAIR_LEARLY
 #define USV_PAIR_LEARLY 5  // the next row's L segment is loaded before the row's chain (not after it) at r <= this
 #endif
@@ -191,7 +188,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * NDMA>();
         __builtin_amdgcn_wave_barrier();
-        if constexpr (USV_PAIR_PRIO && !WARM) __builtin_amdgcn_s_setprio(1);
         // static ring: rows of an unrolled group sit at t = (multiple of WIN) + I, so row t + PD's slot is
         // (I + PD) mod WIN
         constexpr int SLOT_NEXT = C::STATIC ? (I + PD) % NB : -1;
@@ -309,7 +305,6 @@ __device__ __forceinline__ void pair_band_loop(const uint8_t* __restrict__ L, co
         }
         // (after the pending transposed words' lgkmcnt(0) above, which would otherwise wait for it)
         if constexpr (LEARLY) next_lw();
-        if constexpr (USV_PAIR_PRIO && !WARM) __builtin_amdgcn_s_setprio(0);
         // P[j + 1] = P[j] + (|L_j - R(d)| low half, |L_j - R(d + 1)| high half).  With the argmin
         // pipelined, piece j of the previous row's argmin follows chain step j and the pair is
         // fenced: the two independent dependency chains interleave instruction by instruction.
@@ -783,7 +778,6 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
         asm volatile("" : "+s"(t));
         wait_vmcnt<(PD - 1) * C::NQ>();
         __builtin_amdgcn_wave_barrier();
-        if constexpr (USV_PAIR_PRIO && !WARM) __builtin_amdgcn_s_setprio(1);
         constexpr int SLOT_NEXT = (I + PD) % NB;
         if constexpr (WARM) {
             issue_dma(t + PD, SLOT_NEXT);
@@ -812,7 +806,6 @@ __device__ __forceinline__ void pair16_band_loop(const uint8_t* __restrict__ L, 
             }
         }
         issue_reads(i_tag, std::integral_constant<int, K0>{}, std::integral_constant<int, NV>{});
-        if constexpr (USV_PAIR_PRIO && !WARM) __builtin_amdgcn_s_setprio(0);
         auto next_lw = [&] {
             if constexpr (WARM) {
                 load_lw(t + 1);
