@@ -16,7 +16,8 @@
     defined(USV_GROUP_OCC) || defined(USV_GROUP_WEIGHTS) || defined(USV_HIST_KU) ||                              \
     defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_NW2) ||                                        \
     defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) || defined(USV_PAIR_M0REUSE) || defined(USV_PAIR_OCC5) ||              \
-    defined(USV_PAIR_K16) || defined(USV_PAIR_LEARLY) || defined(USV_PAIR16_GEN_WEIGHTS) || defined(USV_PAIR16_RA) || defined(USV_PAIR16_LEARLY) || defined(USV_PAIR16_MIDT) ||                      \
+    defined(USV_PAIR_K16) || defined(USV_PAIR_LEARLY) || defined(USV_PAIR16_GEN_WEIGHTS) ||                      \
+    defined(USV_PAIR16_RA) || defined(USV_PAIR16_LEARLY) || defined(USV_PAIR16_MIDT) ||                          \
     defined(USV_PAIR_OCC7) || defined(USV_PAIR_RDASM) || defined(USV_PREP_KU) || defined(USV_PREP_THREADS) ||    \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_SSD_GEN_WEIGHTS) ||                        \
     defined(USV_SSD_MFMA_MINROWS) || defined(USV_SSD_MFMA_OCC) || defined(USV_SSD_MFMA_WAVES) ||                 \
