@@ -14,6 +14,7 @@
 #ifndef USV_VARIANT_BUILD
 #if defined(USV_GEN_WEIGHTS) || defined(USV_GROUP_MIN_BAND_ROWS) || defined(USV_GROUP_MIN_BAND_WINS) ||          \
     defined(USV_GROUP_OCC) || defined(USV_GROUP_WEIGHTS) || defined(USV_HIST_KU) ||                              \
+    defined(USV_MASK_TH) || defined(USV_MASK_TW) ||                                                              \
     defined(USV_PAIR_GEN_WEIGHTS) || defined(USV_PAIR_GEN_WEIGHTS_NW2) ||                                        \
     defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) || defined(USV_PAIR_M0REUSE) || defined(USV_PAIR_OCC5) ||              \
     defined(USV_PAIR_K16) || defined(USV_PAIR_LEARLY) || defined(USV_PAIR16_GEN_WEIGHTS) ||                      \

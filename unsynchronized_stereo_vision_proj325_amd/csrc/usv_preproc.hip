@@ -407,11 +407,18 @@ __global__ __launch_bounds__(256) void rectify_hsv_hist_kernel(RectPrepJob j0, R
 // in a u32 are processed at once; a shift by k pixels is v_alignbyte over the
 // neighbouring word.  The ellipse is rows -2 and +2 (centre only) and rows
 // -1..1 (five wide): E = T[-2] & T[+2] & h5(T[-1]) & h5(T[0]) & h5(T[+1]).
-constexpr int kTW = 64, kTH = 16;                        // output tile (pixels)
+#ifndef USV_MASK_TW
+#define USV_MASK_TW 64  // output tile width (pixels, multiple of 4); 64 x 16 measured best (profiles/probes_r06/ab_mask_r06.txt)
+#endif
+#ifndef USV_MASK_TH
+#define USV_MASK_TH 16  // output tile height (rows)
+#endif
+constexpr int kTW = USV_MASK_TW, kTH = USV_MASK_TH;       // output tile (pixels)
 constexpr int kR = 2;                                    // ellipse radius
 constexpr int kIH = kTH + 4 * kR, kIWW = (kTW + 8 * kR) / 4 + 0;  // input tile rows, words (4 px halo each side -> 80 px = 20 words)
 constexpr int kEH = kTH + 2 * kR, kEWW = kIWW - 2;      // eroded tile: 20 rows x 18 words (x0 - 4 .. x0 + 67)
 constexpr int kOWW = kTW / 4;                            // 16 output words per row
+constexpr int kMT = kTH * kOWW < 256 ? kTH * kOWW : 256;  // threads per tile: one output word each, at most 256
 
 struct MaskArgs {
     const uint8_t* a;  // gray (motion) or hsv (colour)
@@ -452,12 +459,12 @@ __device__ __forceinline__ int mask_px(const MaskArgs& m, int y, int x) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
+__global__ __launch_bounds__(kMT) void mask_kernel(MaskArgs m, int vec) {
     __shared__ uint32_t T[kIH][kIWW];  // x0 - 8 .. x0 + 71
     __shared__ uint32_t E[kEH][kEWW];  // word e covers x0 - 4 + 4e
     const int X0 = blockIdx.x * kTW, Y0 = blockIdx.y * kTH;
     // thresholded input, rows Y0-4 .. Y0+19, words x0-8 .. x0+71; outside the image = 255 (never wins the min)
-    for (int i = threadIdx.x; i < kIH * kIWW; i += 256) {
+    for (int i = threadIdx.x; i < kIH * kIWW; i += kMT) {
         const int ty = i / kIWW, tw = i - ty * kIWW;
         const int y = Y0 - 2 * kR + ty, x = X0 - 8 + 4 * tw;
         uint32_t w = 0xFFFFFFFFu;
@@ -485,7 +492,7 @@ __global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
     }
     __syncthreads();
     // erode, rows Y0-2 .. Y0+17, words x0-4 .. x0+67; outside the image = 0 (never wins the max)
-    for (int i = threadIdx.x; i < kEH * kEWW; i += 256) {
+    for (int i = threadIdx.x; i < kEH * kEWW; i += kMT) {
         const int ey = i / kEWW, ew = i - ey * kEWW;
         const int y = Y0 - kR + ey, x = X0 - 4 + 4 * ew;
         const int tw = ew + 1, ty = ey + kR;
@@ -500,9 +507,11 @@ __global__ __launch_bounds__(256) void mask_kernel(MaskArgs m, int vec) {
         E[ey][ew] = e;
     }
     __syncthreads();
-    // dilate, one output word (4 pixels) per thread
-    {
-        const int oy = threadIdx.x / kOWW, ow = threadIdx.x - oy * kOWW;
+    // dilate, one output word (4 pixels) per thread and pass
+    static_assert((kTH * kOWW) % kMT == 0, "whole passes of output words");
+#pragma unroll
+    for (int i = threadIdx.x; i < kTH * kOWW; i += kMT) {
+        const int oy = i / kOWW, ow = i - oy * kOWW;
         const int y = Y0 + oy, x = X0 + 4 * ow;
         const int ew = ow + 1, ey = oy + kR;
         const uint32_t d = E[ey - 2][ew] | E[ey + 2][ew] | h5<false>(E[ey - 1], ew) | h5<false>(E[ey], ew) |
@@ -683,7 +692,7 @@ usv_status usv_motion_mask_u8(const uint8_t* gray, const uint8_t* prev, int W, i
     m.mask = mask; m.mask_pitch = mask_pitch;
     dim3 grid((unsigned)((W + usv::kTW - 1) / usv::kTW), (unsigned)((H + usv::kTH - 1) / usv::kTH));
     const int vec = al4(gray) && al4(prev) && al4(mask) && pitch % 4 == 0 && mask_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::mask_kernel<0>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m, vec);
+    hipLaunchKernelGGL(usv::mask_kernel<0>, grid, dim3(usv::kMT), 0, static_cast<hipStream_t>(stream), m, vec);
     return usv::st(hipGetLastError());
 }
 
@@ -699,7 +708,7 @@ usv_status usv_colour_mask_u8(const uint8_t* hsv, int W, int H, int pitch, const
     m.mask = mask; m.mask_pitch = mask_pitch;
     dim3 grid((unsigned)((W + usv::kTW - 1) / usv::kTW), (unsigned)((H + usv::kTH - 1) / usv::kTH));
     const int vec = al4(mask) && mask_pitch % 4 == 0;
-    hipLaunchKernelGGL(usv::mask_kernel<1>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), m, vec);
+    hipLaunchKernelGGL(usv::mask_kernel<1>, grid, dim3(usv::kMT), 0, static_cast<hipStream_t>(stream), m, vec);
     return usv::st(hipGetLastError());
 }
 
