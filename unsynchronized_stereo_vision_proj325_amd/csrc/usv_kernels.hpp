@@ -19,7 +19,8 @@
     defined(USV_PAIR_GEN_WEIGHTS_UNPIPED) || defined(USV_PAIR_M0REUSE) || defined(USV_PAIR_OCC5) ||              \
     defined(USV_PAIR_K16) || defined(USV_PAIR_LEARLY) || defined(USV_PAIR16_GEN_WEIGHTS) ||                      \
     defined(USV_PAIR16_RA) || defined(USV_PAIR16_LEARLY) || defined(USV_PAIR16_MIDT) ||                          \
-    defined(USV_PAIR_OCC7) || defined(USV_PAIR_RDASM) || defined(USV_PREP_KU) || defined(USV_PREP_THREADS) ||    \
+    defined(USV_PAIR_OCC7) || defined(USV_PAIR_RDASM) || defined(USV_PREP_KU) ||                        \
+    defined(USV_PREP_KU_HSV) || defined(USV_PREP_THREADS) ||                                                     \
     defined(USV_REMAP_BLOCK) || defined(USV_REMAP_XCD) || defined(USV_SSD_GEN_WEIGHTS) ||                        \
     defined(USV_SSD_MFMA_MINROWS) || defined(USV_SSD_MFMA_OCC) || defined(USV_SSD_MFMA_WAVES) ||                 \
     defined(USV_STAMPS) || defined(USV_WGTIME)

@@ -89,6 +89,13 @@ static bool fits32(int pitch, int H) { return (long long)pitch * H < (1LL << 31)
 #define USV_PREP_KU 2  // quads per thread per sweep (all their loads issued before any compute)
 #endif
 constexpr int kU = USV_PREP_KU;
+// The equalize pass that reads an HSV image (equalize_kernel<false>: the fused rectify + HSV chain and
+// usv_equalize_hsv_bgr_gray_u8) runs faster at four quads per thread, the one that recomputes HSV from BGR at two
+// (rocprof, three passes: 14.8-15.0 vs 15.6-16.1 us and 14.2-14.5 vs 13.6-13.8 us, profiles/probes_r06/ab_prep_ku_r06.txt).
+#ifndef USV_PREP_KU_HSV
+#define USV_PREP_KU_HSV 4
+#endif
+constexpr int kUHsv = USV_PREP_KU_HSV;
 constexpr int kPT = USV_PREP_THREADS;  // threads per block (frame prep)
 static_assert(kPT % 256 == 0 && kPT <= 1024, "whole 256-bin groups of threads");
 
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(kPT) void equalize_kernel(EqJob j0, EqJob j1, int p
         __syncthreads();
     };
     const bool vec4 = vec && (W & 3) == 0;
-    for_each_quad(
+    for_each_quad<FROM_BGR ? kU : kUHsv>(
         W, H, vec4, (int)blockIdx.x - job * blocks_per_job, blocks_per_job,
         [&](int y, int x, int n, bool v) {
             if constexpr (FROM_BGR) return load_px4(j.src, j.src_pitch, y, x, v, n);
@@ -563,7 +570,7 @@ usv_status usv_equalize_hsv_bgr_gray_u8(const void* work, int parity, uint8_t* h
     const int vec = al4(hsv) && al4(bgr_out) && al4(gray) && hsv_pitch % 4 == 0 && bgr_pitch % 4 == 0 &&
                     gray_pitch % 4 == 0 && usv::fits32(hsv_pitch, H) && usv::fits32(bgr_pitch, H);
     const usv::EqJob j{static_cast<const uint32_t*>(work), hsv, hsv_pitch, bgr_out, bgr_pitch, gray, gray_pitch};
-    const int nb = usv::prep_blocks(W, H);
+    const int nb = usv::prep_blocks(W, H, usv::kUHsv);
     hipLaunchKernelGGL(usv::equalize_kernel<false>, dim3(nb), dim3(usv::kPT), 0, static_cast<hipStream_t>(stream), j, j,
                        parity, W, H, nb, vec);
     return usv::st(hipGetLastError());
@@ -655,7 +662,7 @@ static usv_status rectify_prep_pair(const usv::RemapJob& jl_r, const usv::RemapJ
         hipLaunchKernelGGL(usv::rectify_hsv_hist_kernel<false>, dim3(2 * per_job), dim3(256), 0, s, jl, jr, sW, sH, W,
                            H, per_job, vec_map, vec_src, vec_hsv, parity);
     if (hipGetLastError() != hipSuccess) return USV_ERR_HIP;
-    const int nb = usv::prep_blocks(W, H);
+    const int nb = usv::prep_blocks(W, H, usv::kUHsv);
     hipLaunchKernelGGL(usv::equalize_kernel<false>, dim3(2 * nb), dim3(usv::kPT), 0, s,
                        usv::EqJob{wL, hsvL, hsv_pitch, bgr_outL, bgr_pitch, grayL, gray_pitch},
                        usv::EqJob{wR, hsvR, hsv_pitch, bgr_outR, bgr_pitch, grayR, gray_pitch}, parity, W, H, nb, ve);
